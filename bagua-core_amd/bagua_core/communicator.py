@@ -1,0 +1,99 @@
+"""BaguaSingleCommunicatorPy — RCCL communicator (bagua-core-py/src/lib.rs:14-194).
+
+Creation follows the reference exactly: rank 0 calls the static
+`generate_nccl_unique_id_str()` (base64 of the ncclUniqueId), the caller
+distributes the string (upstream Bagua uses its own store; here any channel,
+e.g. torch.distributed over gloo), and every rank constructs
+`BaguaSingleCommunicatorPy(rank, nranks, device_id, stream_ptr, id)`.
+Collectives are enqueued asynchronously on `stream_ptr`, as in the reference.
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import _native as N
+from .tensor import BaguaTensorPy
+
+
+class BaguaSingleCommunicatorPy:
+    def __init__(self, rank: int, nranks: int, device_id: int, stream_ptr: int, nccl_unique_id_str: str):
+        self._rank, self._nranks, self._device_id = int(rank), int(nranks), int(device_id)
+        self._stream_ptr = int(stream_ptr)
+        handle = N.C.bagua_single_communicator_c_create(self._rank, self._nranks, self._device_id, self._stream_ptr,
+                                                        nccl_unique_id_str.encode())
+        if not handle:
+            raise RuntimeError(f"cannot create RCCL communicator (rank {rank}/{nranks}, device {device_id})")
+        self._handle = ctypes.c_void_p(handle)
+
+    def __del__(self):
+        h = getattr(self, "_handle", None)
+        if h is not None and h.value:
+            N.C.bagua_single_communicator_c_destroy(ctypes.byref(h))
+
+    @staticmethod
+    def generate_nccl_unique_id_str() -> str:
+        buf = ctypes.create_string_buffer(512)
+        N.check(N.C.bagua_generate_nccl_unique_id_str(buf, len(buf)), "ncclGetUniqueId")
+        return buf.value.decode()
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._handle
+
+    def nranks(self) -> int:
+        n = ctypes.c_size_t()
+        N.C.bagua_single_communicator_c_nranks(ctypes.byref(self._handle), ctypes.byref(n))
+        return n.value
+
+    def rank(self) -> int:
+        return self._rank
+
+    def device_id(self) -> int:
+        return self._device_id
+
+    def stream_ptr(self) -> int:
+        return self._stream_ptr
+
+    def abort(self) -> None:
+        N.C.bagua_comm_abort(self._handle)
+
+    def check_abort(self) -> bool:
+        return bool(N.C.bagua_comm_check_abort(self._handle))
+
+    # ---- collectives (communicators/mod.rs:473-1043) --------------------------
+    def _call(self, fn, what, *tensors, extra=()):
+        raws = [t.raw() for t in tensors]
+        N.check(fn(self._handle, *[ctypes.byref(r) for r in raws], *extra), what)
+
+    def allreduce(self, send_tensor: BaguaTensorPy, recv_tensor: BaguaTensorPy, op: int) -> None:
+        self._call(N.C.bagua_comm_allreduce, "allreduce", send_tensor, recv_tensor, extra=(op,))
+
+    def allreduce_inplace(self, tensor: BaguaTensorPy, op: int) -> None:
+        self._call(N.C.bagua_comm_allreduce_inplace, "allreduce_inplace", tensor, extra=(op,))
+
+    def broadcast(self, tensor: BaguaTensorPy, root_rank: int) -> None:
+        self._call(N.C.bagua_comm_broadcast, "broadcast", tensor, extra=(root_rank,))
+
+    def send(self, tensor: BaguaTensorPy, peer_rank: int) -> None:
+        self._call(N.C.bagua_comm_send, "send", tensor, extra=(peer_rank,))
+
+    def recv(self, tensor: BaguaTensorPy, peer_rank: int) -> None:
+        self._call(N.C.bagua_comm_recv, "recv", tensor, extra=(peer_rank,))
+
+    def alltoall(self, send_tensor: BaguaTensorPy, recv_tensor: BaguaTensorPy) -> None:
+        self._call(N.C.bagua_comm_alltoall, "alltoall", send_tensor, recv_tensor)
+
+    def alltoall_inplace(self, tensor: BaguaTensorPy) -> None:
+        self._call(N.C.bagua_comm_alltoall_inplace, "alltoall_inplace", tensor)
+
+    def allgather(self, send_tensor: BaguaTensorPy, recv_tensor: BaguaTensorPy) -> None:
+        self._call(N.C.bagua_comm_allgather, "allgather", send_tensor, recv_tensor)
+
+    def allgather_inplace(self, tensor: BaguaTensorPy) -> None:
+        self._call(N.C.bagua_comm_allgather_inplace, "allgather_inplace", tensor)
+
+    def barrier(self) -> None:
+        N.check(N.C.bagua_comm_barrier(self._handle), "barrier")
+
+    def synchronize(self) -> None:
+        N.check(N.C.bagua_comm_synchronize(self._handle), "stream synchronize")

@@ -1,0 +1,36 @@
+// launch_util.hpp — host-side launch helpers shared by the kernel TUs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "bagua_kernels.h"
+
+namespace bagua {
+
+// 256 CUs x 8 resident 256-thread workgroups: enough waves in flight to
+// cover HBM latency on a streaming kernel; larger problems grid-stride.
+constexpr int kTargetBlocks = 2048;
+
+// last hipError_t seen by a launcher on this thread (bagua_last_hip_error)
+extern thread_local int g_last_hip_error;
+
+inline int check_launch() {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_last_hip_error = (int)e;
+        return BAGUA_ERR_HIP;
+    }
+    return BAGUA_OK;
+}
+
+// v1 convention: CUDACHECK prints and exits (bagua-core-internal/cpp/include/bagua_utils.h:5)
+inline void v1_check(int status, const char* file, int line) {
+    if (status != BAGUA_OK) {
+        printf("Failed: bagua kernel error %s:%d '%s'\n", file, line, bagua_status_string(status));
+        exit(EXIT_FAILURE);
+    }
+}
+
+}  // namespace bagua

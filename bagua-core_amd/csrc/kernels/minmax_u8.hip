@@ -1,0 +1,460 @@
+// minmax_u8.hip — MinMax-UInt8 gradient codec for gfx950 (MI355X).
+//
+// Replaces the reference's per-chunk cub::DeviceReduce::Min + ::Max passes
+// (bagua_kernels.cu:312-371, 2p serial launches) and the scalar
+// compress/decompress kernels (bagua_kernels.cu:455-500, 4-byte loads /
+// 1-byte stores, 1024-thread blocks) with three streaming kernels:
+//
+//   minmax_partials  : one read of the chunk, 16-B loads, fused min AND max,
+//                      wave64 shuffles + LDS, one partial per workgroup
+//   minmax_quantize  : folds the partials (L2-resident, tiny), writes the
+//                      header, quantises with 16-B loads / 4-B or 8-B stores;
+//                      sweeps the chunk in REVERSE so the tail the previous
+//                      kernel just streamed is re-read from the 256 MiB
+//                      Infinity Cache first
+//   minmax_dequantize: 4/8-B loads, 16-B stores
+//
+// Payload bytes and header values are bit-identical to the reference
+// expressions (see codec_common.hpp); NaN / signed-zero handling of the
+// min/max is pinned order-independently.
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "codec_common.hpp"
+#include "launch_util.hpp"
+
+namespace bagua {
+
+constexpr int kVecPerBlockTile = kBlock * kSubtiles;  // 1024 x 16-B vectors = 16 KiB in flight per block
+
+__device__ __forceinline__ int64_t chunk_valid(int64_t in_num_elem, int64_t cs, int c) {
+    // K:538-545: remaining elements, clamped to [0, chunk_size]
+    int64_t r = in_num_elem - (int64_t)c * cs;
+    return r < 0 ? 0 : (r < cs ? r : cs);
+}
+
+template <typename T>
+__device__ __forceinline__ void fold(float f, uint32_t& lo, uint32_t& hi) {
+    const int32_t k = f2key(f);
+    lo = min(lo, (uint32_t)(k - kKeyNegInf));
+    hi = min(hi, (uint32_t)(kKeyPosInf - k));
+}
+
+// ------------------------------------------------------------------------
+// pass 1: per-workgroup partial min/max of each active chunk
+// ------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock) void minmax_partials_kernel(
+    const typename T::storage* __restrict__ in, int64_t in_num_elem, int64_t cs, int target,
+    uint2* __restrict__ partials) {
+    using S = typename T::storage;
+    constexpr int N = Vec<T>::N;
+    const int c = target < 0 ? (int)blockIdx.y : target;
+    const int64_t n = chunk_valid(in_num_elem, cs, c);
+    const S* src = in + (int64_t)c * cs;
+
+    int64_t j0 = (int64_t)(((16u - ((uintptr_t)src & 15u)) & 15u) / sizeof(S));
+    if (j0 > n) j0 = n;
+    const int64_t nvec = (n - j0) / N;
+    const uint4* __restrict__ vsrc = reinterpret_cast<const uint4*>(src + j0);
+
+    uint32_t lo = min_space(T::init_max());
+    uint32_t hi = max_space(-T::init_max());
+    const int64_t stride = (int64_t)gridDim.x * kVecPerBlockTile;
+    for (int64_t base = (int64_t)blockIdx.x * kVecPerBlockTile; base < nvec; base += stride) {
+        uint4 r[kSubtiles];
+        bool ok[kSubtiles];
+#pragma unroll
+        for (int k = 0; k < kSubtiles; ++k) {
+            const int64_t v = base + k * kBlock + threadIdx.x;
+            ok[k] = v < nvec;
+            if (ok[k]) r[k] = vsrc[v];  // default policy: pass 2 re-reads these lines
+        }
+#pragma unroll
+        for (int k = 0; k < kSubtiles; ++k) {
+            if (!ok[k]) continue;
+            float f[N];
+            unpack16<T>(r[k], f);
+#pragma unroll
+            for (int i = 0; i < N; ++i) fold<T>(f[i], lo, hi);
+        }
+    }
+    if (blockIdx.x == 0) {  // unaligned head and ragged tail (< 2N elements)
+        for (int64_t j = threadIdx.x; j < j0; j += kBlock) fold<T>(T::to_f(src[j]), lo, hi);
+        for (int64_t j = j0 + nvec * N + threadIdx.x; j < n; j += kBlock) fold<T>(T::to_f(src[j]), lo, hi);
+    }
+
+    lo = wave_umin(lo);
+    hi = wave_umin(hi);
+    __shared__ uint32_t red[2][kWavesPerBlock];
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 0) { red[0][w] = lo; red[1][w] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 1; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
+        partials[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = make_uint2(lo, hi);
+    }
+}
+
+// ------------------------------------------------------------------------
+// pass 2: fold partials, write header, quantise
+// ------------------------------------------------------------------------
+template <typename T, bool kReverse>
+__global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
+    const typename T::storage* __restrict__ in, int64_t in_num_elem, int64_t cs, int target,
+    const uint2* __restrict__ partials, int npartials, uint8_t* __restrict__ out,
+    int64_t chunk_offset, int64_t out_bytes, int num_chunks) {
+    using S = typename T::storage;
+    constexpr int N = Vec<T>::N;
+    const int cidx = kReverse ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
+    const int c = target < 0 ? cidx : target;
+    const int64_t n = chunk_valid(in_num_elem, cs, c);
+    const S* src = in + (int64_t)c * cs;
+    uint8_t* seg = out + (int64_t)c * chunk_offset;
+
+    // fold the chunk's partials (written by pass 1; L2/MALL-resident)
+    uint32_t lo = 0xffffffffu, hi = 0xffffffffu;
+    for (int i = threadIdx.x; i < npartials; i += kBlock) {
+        const uint2 p = partials[(int64_t)cidx * npartials + i];
+        lo = min(lo, p.x);
+        hi = min(hi, p.y);
+    }
+    lo = wave_umin(lo);
+    hi = wave_umin(hi);
+    __shared__ uint32_t red[2][kWavesPerBlock];
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 0) { red[0][w] = lo; red[1][w] = hi; }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
+    // the header holds T values (K:462-463); min/max of T data are exact in T
+    const float mn = from_min_space(lo), mx = from_max_space(hi);
+    const QParams q = make_qparams(mn, mx);
+
+    if (blockIdx.x == 0) {
+        // header {T min, T max, zero gap} (reference leaves the gap uninitialised)
+        if (threadIdx.x < 32) {
+            uint32_t hb = 0;
+            const uint32_t bmn = sizeof(S) == 4 ? __float_as_uint(mn) : (uint32_t)T::from_f(mn);
+            const uint32_t bmx = sizeof(S) == 4 ? __float_as_uint(mx) : (uint32_t)T::from_f(mx);
+            const int t = threadIdx.x;
+            if (t < (int)sizeof(S)) hb = (bmn >> (8 * t)) & 0xff;
+            else if (t < 2 * (int)sizeof(S)) hb = (bmx >> (8 * (t - (int)sizeof(S)))) & 0xff;
+            seg[t] = (uint8_t)hb;
+        }
+        // slack after the payload, and the buffer tail after the last segment
+        for (int64_t j = 32 + cs + threadIdx.x; j < chunk_offset; j += kBlock) seg[j] = 0;
+        if (target < 0 && c == num_chunks - 1)
+            for (int64_t j = (int64_t)num_chunks * chunk_offset + threadIdx.x; j < out_bytes; j += kBlock)
+                out[j] = 0;
+    }
+
+    uint8_t* payload = seg + 32;
+    const int a = common_alignment<T>((uintptr_t)src, (uintptr_t)payload);
+    if (a < 0) {  // no common vector alignment: scalar path over the whole chunk
+        for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < cs; j += (int64_t)gridDim.x * kBlock)
+            payload[j] = (uint8_t)(j < n ? quant(T::to_f(src[j]), q) : 0u);
+        return;
+    }
+    const int64_t j0 = a < cs ? a : cs;
+    const int64_t nvec = (cs - j0) / N;
+    const uint4* __restrict__ vsrc = reinterpret_cast<const uint4*>(src + j0);
+    uint8_t* vdst = payload + j0;
+    const int64_t ntiles = (nvec + kVecPerBlockTile - 1) / kVecPerBlockTile;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int64_t base = (kReverse ? (ntiles - 1 - t) : t) * kVecPerBlockTile;
+        uint4 r[kSubtiles];
+        bool ok[kSubtiles];
+#pragma unroll
+        for (int k = 0; k < kSubtiles; ++k) {
+            const int64_t v = base + k * kBlock + threadIdx.x;
+            ok[k] = v < nvec;
+            if (ok[k]) r[k] = nt_load16(&vsrc[v]);
+        }
+#pragma unroll
+        for (int k = 0; k < kSubtiles; ++k) {
+            if (!ok[k]) continue;
+            const int64_t v = base + k * kBlock + threadIdx.x;
+            float f[N];
+            unpack16<T>(r[k], f);
+            uint32_t b[N];
+            const int64_t jv = j0 + v * N;
+#pragma unroll
+            for (int i = 0; i < N; ++i) b[i] = (jv + i < n) ? quant(f[i], q) : 0u;
+            store_bytes<T>(vdst + v * N, b);
+        }
+    }
+    if (blockIdx.x == 0) {
+        for (int64_t j = threadIdx.x; j < j0; j += kBlock)
+            payload[j] = (uint8_t)(j < n ? quant(T::to_f(src[j]), q) : 0u);
+        for (int64_t j = j0 + nvec * N + threadIdx.x; j < cs; j += kBlock)
+            payload[j] = (uint8_t)(j < n ? quant(T::to_f(src[j]), q) : 0u);
+    }
+}
+
+// ------------------------------------------------------------------------
+// dequantise
+// ------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
+    const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs,
+    typename T::storage* __restrict__ out) {
+    using S = typename T::storage;
+    constexpr int N = Vec<T>::N;
+    const int c = blockIdx.y;
+    const uint8_t* seg = in + (int64_t)c * chunk_offset;
+    const QParams q = read_header<T>(seg);
+    const uint8_t* payload = seg + 32;
+    S* dst = out + (int64_t)c * cs;
+
+    const int a = common_alignment<T>((uintptr_t)dst, (uintptr_t)payload);
+    if (a < 0) {
+        for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < cs; j += (int64_t)gridDim.x * kBlock)
+            dst[j] = T::from_f(dequant(payload[j], q));
+        return;
+    }
+    const int64_t j0 = a < cs ? a : cs;
+    const int64_t nvec = (cs - j0) / N;
+    uint4* __restrict__ vdst = reinterpret_cast<uint4*>(dst + j0);
+    const uint8_t* vsrc = payload + j0;
+    const int64_t stride = (int64_t)gridDim.x * kVecPerBlockTile;
+    for (int64_t base = (int64_t)blockIdx.x * kVecPerBlockTile; base < nvec; base += stride) {
+        uint32_t b[kSubtiles][N];
+        bool ok[kSubtiles];
+#pragma unroll
+        for (int k = 0; k < kSubtiles; ++k) {
+            const int64_t v = base + k * kBlock + threadIdx.x;
+            ok[k] = v < nvec;
+            if (ok[k]) load_bytes<T>(vsrc + v * N, b[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < kSubtiles; ++k) {
+            if (!ok[k]) continue;
+            const int64_t v = base + k * kBlock + threadIdx.x;
+            float f[N];
+#pragma unroll
+            for (int i = 0; i < N; ++i) f[i] = dequant(b[k][i], q);
+            nt_store16(pack16<T>(f), &vdst[v]);
+        }
+    }
+    if (blockIdx.x == 0) {
+        for (int64_t j = threadIdx.x; j < j0; j += kBlock) dst[j] = T::from_f(dequant(payload[j], q));
+        for (int64_t j = j0 + nvec * N + threadIdx.x; j < cs; j += kBlock)
+            dst[j] = T::from_f(dequant(payload[j], q));
+    }
+}
+
+// ------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------
+static int blocks_for(int64_t elems, int per_vec, int nact) {
+    const int64_t nvec = elems / per_vec + 1;
+    int64_t tiles = (nvec + kVecPerBlockTile - 1) / kVecPerBlockTile;
+    const int64_t per_chunk = (kTargetBlocks + nact - 1) / nact;
+    if (tiles > per_chunk) tiles = per_chunk;
+    return (int)(tiles < 1 ? 1 : tiles);
+}
+
+// stage bit 1: min/max partials pass; bit 2: quantise pass (3 = whole compress).
+// Both stages derive the same partials count from the same arguments.
+template <typename T>
+static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint8_t* out,
+                         size_t out_bytes, void* ws, size_t ws_bytes, int target, hipStream_t s,
+                         int stages = 3) {
+    using S = typename T::storage;
+    if (p <= 0 || p > 65535 || cs < 0 || target < -1 || target >= p || !input || !out)
+        return BAGUA_ERR_INVALID_ARG;
+    const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);  // K:537
+    if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
+    const int nact = target < 0 ? p : 1;
+    int nblk = blocks_for(cs, Vec<T>::N, nact);
+    const int64_t cap = ws ? (int64_t)(ws_bytes / sizeof(uint2)) / nact : 0;
+    if (cap < 1) return BAGUA_ERR_WORKSPACE;
+    if (nblk > cap) nblk = (int)cap;
+    uint2* partials = static_cast<uint2*>(ws);
+    if (stages & 1)
+        hipLaunchKernelGGL(minmax_partials_kernel<T>, dim3(nblk, nact), dim3(kBlock), 0, s,
+                           static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, partials);
+    if (stages & 2)
+        hipLaunchKernelGGL((minmax_quantize_kernel<T, true>), dim3(blocks_for(cs, Vec<T>::N, nact), nact),
+                           dim3(kBlock), 0, s, static_cast<const S*>(input), (int64_t)in_num_elem,
+                           (int64_t)cs, target, partials, nblk, out, chunk_offset, (int64_t)out_bytes, p);
+    return check_launch();
+}
+
+// defined in reduce.hip
+int fused_blocks(int64_t cs, int per_vec);
+template <typename T>
+int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, int average, uint2* partials,
+                        int blocks, hipStream_t s);
+
+template <typename T>
+static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, void* tensor, int average,
+                                  uint8_t* out, size_t out_bytes, int target, void* ws, size_t ws_bytes,
+                                  hipStream_t s) {
+    using S = typename T::storage;
+    if (p <= 0 || p > kMaxFusedChunks || cs < 0 || target < 0 || target >= p || !tensor || !out)
+        return BAGUA_ERR_UNSUPPORTED;
+    const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);
+    if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
+    const int blocks = fused_blocks(cs, Vec<T>::N);
+    if (!ws || ws_bytes < (size_t)blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
+    S* chunk = static_cast<S*>(tensor) + (int64_t)target * cs;
+    uint2* partials = static_cast<uint2*>(ws);
+    int rc = dequant_reduce_impl<T>(recv, recv_bytes, cs, p, chunk, average, partials, blocks, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL((minmax_quantize_kernel<T, true>), dim3(blocks_for(cs, Vec<T>::N, 1), 1), dim3(kBlock), 0, s,
+                       static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, target, partials, blocks, out,
+                       chunk_offset, (int64_t)out_bytes, p);
+    return check_launch();
+}
+
+template <typename T>
+static int decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, hipStream_t s) {
+    using S = typename T::storage;
+    if (p <= 0 || p > 65535 || cs < 0 || !in || !out) return BAGUA_ERR_INVALID_ARG;
+    const int64_t chunk_offset = (int64_t)(in_bytes / (size_t)p);  // K:566
+    if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
+    hipLaunchKernelGGL(minmax_dequantize_kernel<T>, dim3(blocks_for(cs, Vec<T>::N, p), p), dim3(kBlock), 0,
+                       s, in, chunk_offset, (int64_t)cs, static_cast<S*>(out));
+    return check_launch();
+}
+
+}  // namespace bagua
+
+using namespace bagua;
+
+extern "C" {
+
+size_t bagua_minmax_u8_compressed_bytes(int dtype, int chunk_size, int num_chunks) {
+    // datatypes/mod.rs:669-704
+    const size_t esz = dtype == BAGUA_DTYPE_F32 ? 4 : 2;
+    auto al = [](size_t x, size_t a) { return (x + a - 1) / a * a; };
+    return al((size_t)chunk_size * (size_t)num_chunks, 32) + al(2 * esz, 32) * (size_t)num_chunks;
+}
+
+size_t bagua_minmax_u8_workspace_bytes(int /*chunk_size*/, int num_chunks) {
+    // one uint2 partial per workgroup; at most kTargetBlocks + num_chunks workgroups
+    return sizeof(uint2) * ((size_t)kTargetBlocks + (size_t)(num_chunks > 0 ? num_chunks : 1)) + 256;
+}
+
+int bagua_minmax_u8_compress(int dtype, const void* input, int input_num_element, int chunk_size,
+                             int num_chunks, uint8_t* output, size_t output_bytes, void* workspace,
+                             size_t workspace_bytes, int target_chunk, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return compress_impl<F32>(input, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                      workspace, workspace_bytes, target_chunk, s);
+        case BAGUA_DTYPE_F16:
+            return compress_impl<F16>(input, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                      workspace, workspace_bytes, target_chunk, s);
+        case BAGUA_DTYPE_BF16:
+            return compress_impl<BF16>(input, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                       workspace, workspace_bytes, target_chunk, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+int bagua_minmax_u8_decompress(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                               int num_chunks, void* output, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32: return decompress_impl<F32>(input, input_bytes, chunk_size, num_chunks, output, s);
+        case BAGUA_DTYPE_F16: return decompress_impl<F16>(input, input_bytes, chunk_size, num_chunks, output, s);
+        case BAGUA_DTYPE_BF16: return decompress_impl<BF16>(input, input_bytes, chunk_size, num_chunks, output, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+int bagua_minmax_u8_compress_stage(int stage, int dtype, const void* input, int input_num_element, int chunk_size,
+                                   int num_chunks, uint8_t* output, size_t output_bytes, void* workspace,
+                                   size_t workspace_bytes, int target_chunk, bagua_stream_t stream) {
+    if (stage != 1 && stage != 2) return BAGUA_ERR_INVALID_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return compress_impl<F32>(input, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                      workspace, workspace_bytes, target_chunk, s, stage);
+        case BAGUA_DTYPE_F16:
+            return compress_impl<F16>(input, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                      workspace, workspace_bytes, target_chunk, s, stage);
+        case BAGUA_DTYPE_BF16:
+            return compress_impl<BF16>(input, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                       workspace, workspace_bytes, target_chunk, s, stage);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+int bagua_minmax_u8_reduce_requantize(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                                      int num_chunks, void* tensor, int average, uint8_t* output, size_t output_bytes,
+                                      int target_chunk, void* workspace, size_t workspace_bytes,
+                                      bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return reduce_requantize_impl<F32>(input, input_bytes, chunk_size, num_chunks, tensor, average, output,
+                                               output_bytes, target_chunk, workspace, workspace_bytes, s);
+        case BAGUA_DTYPE_F16:
+            return reduce_requantize_impl<F16>(input, input_bytes, chunk_size, num_chunks, tensor, average, output,
+                                               output_bytes, target_chunk, workspace, workspace_bytes, s);
+        case BAGUA_DTYPE_BF16:
+            return reduce_requantize_impl<BF16>(input, input_bytes, chunk_size, num_chunks, tensor, average, output,
+                                                output_bytes, target_chunk, workspace, workspace_bytes, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+// ---- v1 surface (bagua_kernels.cu:661-689) --------------------------------
+void compress_f32_to_uint8_host(float* input, int input_num_element, int chunk_size, int num_chunks,
+                                uint8_t* output, size_t output_size, void* dev_buffer, size_t dev_size,
+                                int target_chunk, bagua_stream_t stream) {
+    v1_check(bagua_minmax_u8_compress(BAGUA_DTYPE_F32, input, input_num_element, chunk_size, num_chunks,
+                                      output, output_size, dev_buffer, dev_size, target_chunk, stream),
+             __FILE__, __LINE__);
+}
+void compress_f16_to_uint8_host(bagua_half_t* input, int input_num_element, int chunk_size, int num_chunks,
+                                uint8_t* output, size_t output_size, void* dev_buffer, size_t dev_size,
+                                int target_chunk, bagua_stream_t stream) {
+    v1_check(bagua_minmax_u8_compress(BAGUA_DTYPE_F16, input, input_num_element, chunk_size, num_chunks,
+                                      output, output_size, dev_buffer, dev_size, target_chunk, stream),
+             __FILE__, __LINE__);
+}
+void compress_bf16_to_uint8_host(bagua_bf16_t* input, int input_num_element, int chunk_size, int num_chunks,
+                                 uint8_t* output, size_t output_size, void* dev_buffer, size_t dev_size,
+                                 int target_chunk, bagua_stream_t stream) {
+    v1_check(bagua_minmax_u8_compress(BAGUA_DTYPE_BF16, input, input_num_element, chunk_size, num_chunks,
+                                      output, output_size, dev_buffer, dev_size, target_chunk, stream),
+             __FILE__, __LINE__);
+}
+void decompress_uint8_to_f32_host(uint8_t* input, size_t input_size, int chunk_size, int num_chunks,
+                                  float* output, bagua_stream_t stream) {
+    v1_check(bagua_minmax_u8_decompress(BAGUA_DTYPE_F32, input, input_size, chunk_size, num_chunks, output,
+                                        stream),
+             __FILE__, __LINE__);
+}
+void decompress_uint8_to_f16_host(uint8_t* input, size_t input_size, int chunk_size, int num_chunks,
+                                  bagua_half_t* output, bagua_stream_t stream) {
+    v1_check(bagua_minmax_u8_decompress(BAGUA_DTYPE_F16, input, input_size, chunk_size, num_chunks, output,
+                                        stream),
+             __FILE__, __LINE__);
+}
+void decompress_uint8_to_bf16_host(uint8_t* input, size_t input_size, int chunk_size, int num_chunks,
+                                   bagua_bf16_t* output, bagua_stream_t stream) {
+    v1_check(bagua_minmax_u8_decompress(BAGUA_DTYPE_BF16, input, input_size, chunk_size, num_chunks, output,
+                                        stream),
+             __FILE__, __LINE__);
+}
+// K:683-689: the reference returns cub's temp bytes; here: our partials workspace
+size_t array_min_max_size_f32_host(float*, int, float*, bagua_stream_t) {
+    return bagua_minmax_u8_workspace_bytes(0, kTargetBlocks);
+}
+size_t array_min_max_size_f16_host(bagua_half_t*, int, bagua_half_t*, bagua_stream_t) {
+    return bagua_minmax_u8_workspace_bytes(0, kTargetBlocks);
+}
+size_t array_min_max_size_bf16_host(bagua_bf16_t*, int, bagua_bf16_t*, bagua_stream_t) {
+    return bagua_minmax_u8_workspace_bytes(0, kTargetBlocks);
+}
+
+}  // extern "C"

@@ -1,0 +1,345 @@
+// onebit.hip — 1-bit sign + scale gradient codec for gfx950 (extension; the
+// reference has only MinMaxUInt8).  Format: DESIGN.md §4.
+//
+// The bit layout is wave-native: one wave owns a 1024-element tile; element
+// r = sub*256 + lane*4 + e of the tile is bit `lane` of u64 word (sub*4+e),
+// so encoding a tile is 16 __ballot()s (v_cmp straight into an SGPR pair)
+// and decoding is 32 v_readlane + a shift per element — no LDS, no
+// cross-lane packing.  Loads/stores stay 16-B (f32) / 8-B (16-bit) per lane,
+// fully coalesced.
+//
+// scale = mean(|x|) with a FIXED summation tree (lane-local pairs, then a
+// 64-lane xor butterfly per tile, then the same 1024-tree over the tile
+// partials), so the encoder is single-pass over the input and its result is
+// independent of grid size and bit-reproducible against the oracle.
+#include "codec_common.hpp"
+#include "launch_util.hpp"
+
+namespace bagua {
+
+constexpr int kObTile = 1024;
+constexpr int kObTileBytes = 128;
+constexpr int kObFinalizeThreads = 1024;
+
+__device__ __forceinline__ int64_t ob_valid(int64_t in_num_elem, int64_t cs, int c) {
+    int64_t r = in_num_elem - (int64_t)c * cs;
+    return r < 0 ? 0 : (r < cs ? r : cs);
+}
+
+// 4 consecutive elements of T starting at p (vector load when 4*sizeof(T)-aligned)
+template <typename T>
+__device__ __forceinline__ void load4(const typename T::storage* p, int64_t j, int64_t n, bool vec, float (&f)[4]) {
+    using S = typename T::storage;
+    if (vec && j + 4 <= n) {
+        if constexpr (sizeof(S) == 4) {
+            const uint4 v = nt_load16(p + j);
+            f[0] = __uint_as_float(v.x); f[1] = __uint_as_float(v.y);
+            f[2] = __uint_as_float(v.z); f[3] = __uint_as_float(v.w);
+        } else {
+            const uint2 v = nt_load8(p + j);
+            f[0] = T::to_f((uint16_t)(v.x & 0xffff)); f[1] = T::to_f((uint16_t)(v.x >> 16));
+            f[2] = T::to_f((uint16_t)(v.y & 0xffff)); f[3] = T::to_f((uint16_t)(v.y >> 16));
+        }
+        return;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f[e] = (j + e < n) ? T::load(p, j + e) : 0.0f;
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(typename T::storage* p, int64_t j, int64_t n, bool vec, const float (&f)[4]) {
+    using S = typename T::storage;
+    if (vec && j + 4 <= n) {
+        if constexpr (sizeof(S) == 4) {
+            nt_store16(make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3])), p + j);
+        } else {
+            uint2 v;
+            v.x = (uint32_t)T::from_f(f[0]) | ((uint32_t)T::from_f(f[1]) << 16);
+            v.y = (uint32_t)T::from_f(f[2]) | ((uint32_t)T::from_f(f[3]) << 16);
+            nt_store8(v, p + j);
+        }
+        return;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (j + e < n) p[j + e] = T::from_f(f[e]);
+}
+
+// the 64-lane tree of the tile sum: s[l] += s[l^h], h = 32..1 (== s[l] + s[l+h])
+__device__ __forceinline__ float wave_tree_sum(float s) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s = s + __shfl_xor(s, o, kWave);
+    return s;
+}
+
+// lane-local part of the tile tree for values a[sub][e]
+__device__ __forceinline__ float lane_tree(const float (&a)[4][4]) {
+    float q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = (a[k][0] + a[k][1]) + (a[k][2] + a[k][3]);
+    return (q[0] + q[1]) + (q[2] + q[3]);
+}
+
+// ------------------------------------------------------------------------
+// encode: bits + per-tile |x| partials, one wave per tile
+// ------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
+    const typename T::storage* __restrict__ in, int64_t in_num_elem, int64_t cs, int target,
+    uint8_t* __restrict__ out, int64_t chunk_offset, float* __restrict__ partials, int64_t tiles_per_chunk) {
+    using S = typename T::storage;
+    const int c = target < 0 ? (int)blockIdx.y : target;
+    const int64_t n = ob_valid(in_num_elem, cs, c);
+    const S* src = in + (int64_t)c * cs;
+    const bool vec = ((uintptr_t)src % (4 * sizeof(S))) == 0;
+    uint8_t* bits = out + (int64_t)c * chunk_offset + 32;
+    float* part = partials + (int64_t)blockIdx.y * tiles_per_chunk;
+    const int lane = lane_id();
+    const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t t = wave; t < tiles_per_chunk; t += nwaves) {
+        float a[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) load4<T>(src, t * kObTile + k * 256 + lane * 4, n, vec, a[k]);
+        uint32_t word = 0;  // lane l < 32 stores dword l of the 128-byte tile
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint64_t m = __ballot(a[k][e] < 0.0f);
+                const int w = k * 4 + e;
+                if ((lane >> 1) == w) word = (lane & 1) ? (uint32_t)(m >> 32) : (uint32_t)m;
+            }
+        if (lane < 32) reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane] = word;
+        float ab[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ab[k][e] = __builtin_fabsf(a[k][e]);
+        const float s = wave_tree_sum(lane_tree(ab));
+        if (lane == 0) part[t] = s;
+    }
+}
+
+// ------------------------------------------------------------------------
+// finalize: scale = F(partials) / n, header, slack (one workgroup per chunk)
+// ------------------------------------------------------------------------
+__device__ __forceinline__ float tile_from(const float* v, int64_t base, int64_t count, int lane) {
+    float a[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t r = base + k * 256 + lane * 4 + e;
+            a[k][e] = r < count ? v[r] : 0.0f;
+        }
+    return wave_tree_sum(lane_tree(a));
+}
+
+__global__ __launch_bounds__(kObFinalizeThreads) void onebit_finalize_kernel(
+    const float* __restrict__ partials, int64_t tiles_per_chunk, int64_t in_num_elem, int64_t cs, int target,
+    uint8_t* __restrict__ out, int64_t chunk_offset, int64_t out_bytes, int num_chunks) {
+    __shared__ float lvl[2][2048];  // level >= 2 values: <= ceil(2^21 / 1024)
+    const int c = target < 0 ? (int)blockIdx.x : target;
+    const int64_t n = ob_valid(in_num_elem, cs, c);
+    const float* part = partials + (int64_t)blockIdx.x * tiles_per_chunk;
+    const int64_t m1 = (n + kObTile - 1) / kObTile;  // tiles holding valid elements
+    const int lane = lane_id(), wave = threadIdx.x / kWave, nw = kObFinalizeThreads / kWave;
+    float total = 0.0f;
+    if (m1 > 0) {
+        // level 1 -> 2 from global memory
+        int64_t m = m1;
+        const int64_t g1 = (m + kObTile - 1) / kObTile;
+        for (int64_t g = wave; g < g1; g += nw) {
+            const float s = tile_from(part, g * kObTile, m, lane);
+            if (lane == 0) lvl[0][g] = s;
+        }
+        __syncthreads();
+        int cur = 0;
+        bool done = m <= kObTile;
+        m = g1;
+        while (!done) {
+            const int64_t g = (m + kObTile - 1) / kObTile;
+            for (int64_t i = wave; i < g; i += nw) {
+                const float s = tile_from(lvl[cur], i * kObTile, m, lane);
+                if (lane == 0) lvl[cur ^ 1][i] = s;
+            }
+            __syncthreads();
+            done = m <= kObTile;
+            cur ^= 1;
+            m = g;
+        }
+        total = lvl[cur][0];
+    }
+    uint8_t* seg = out + (int64_t)c * chunk_offset;
+    if (threadIdx.x < 32) {
+        const float scale = n > 0 ? total / (float)n : 0.0f;
+        const uint32_t sb = __float_as_uint(scale), nb = (uint32_t)n;
+        const int t = threadIdx.x;
+        uint32_t b = 0;
+        if (t < 4) b = (sb >> (8 * t)) & 0xff;
+        else if (t < 8) b = (nb >> (8 * (t - 4))) & 0xff;
+        seg[t] = (uint8_t)b;
+    }
+    const int64_t tiles = (cs + kObTile - 1) / kObTile;
+    for (int64_t j = 32 + tiles * kObTileBytes + threadIdx.x; j < chunk_offset; j += kObFinalizeThreads) seg[j] = 0;
+    if (target < 0 && c == num_chunks - 1)
+        for (int64_t j = (int64_t)num_chunks * chunk_offset + threadIdx.x; j < out_bytes; j += kObFinalizeThreads)
+            out[j] = 0;
+}
+
+// ------------------------------------------------------------------------
+// decode
+// ------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock) void onebit_decode_kernel(const uint8_t* __restrict__ in, int64_t chunk_offset,
+                                                              int64_t cs, typename T::storage* __restrict__ out) {
+    using S = typename T::storage;
+    const int c = blockIdx.y;
+    const uint8_t* seg = in + (int64_t)c * chunk_offset;
+    float scale;
+    __builtin_memcpy(&scale, seg, 4);
+    const uint8_t* bits = seg + 32;
+    S* dst = out + (int64_t)c * cs;
+    const bool vec = ((uintptr_t)dst % (4 * sizeof(S))) == 0;
+    const int lane = lane_id();
+    const int64_t tiles = (cs + kObTile - 1) / kObTile;
+    const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t t = wave; t < tiles; t += nwaves) {
+        const uint32_t mine = lane < 32 ? reinterpret_cast<const uint32_t*>(bits + t * kObTileBytes)[lane] : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float f[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int w = k * 4 + e;
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2 * w);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2 * w + 1);
+                const uint32_t word = lane < 32 ? lo : hi;
+                f[e] = ((word >> (lane & 31)) & 1u) ? -scale : scale;
+            }
+            store4<T>(dst, t * kObTile + k * 256 + lane * 4, cs, vec, f);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// host
+// ------------------------------------------------------------------------
+static int64_t ob_tiles(int64_t cs) { return (cs + kObTile - 1) / kObTile; }
+
+static int ob_blocks(int64_t tiles, int nact) {
+    int64_t b = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int64_t cap = (kTargetBlocks + nact - 1) / nact;
+    if (b > cap) b = cap;
+    return (int)(b < 1 ? 1 : b);
+}
+
+template <typename T>
+static int ob_compress_impl(const void* input, int in_num_elem, int cs, int p, uint8_t* out, size_t out_bytes,
+                            void* ws, size_t ws_bytes, int target, hipStream_t s) {
+    using S = typename T::storage;
+    if (p <= 0 || p > 65535 || cs < 0 || target < -1 || target >= p || !input || !out) return BAGUA_ERR_INVALID_ARG;
+    const int64_t co = (int64_t)(out_bytes / (size_t)p);
+    const int64_t tiles = ob_tiles(cs);
+    if (co < 32 + tiles * kObTileBytes) return BAGUA_ERR_INVALID_ARG;
+    const int nact = target < 0 ? p : 1;
+    if (!ws || ws_bytes < (size_t)nact * (size_t)(tiles > 0 ? tiles : 1) * sizeof(float)) return BAGUA_ERR_WORKSPACE;
+    if (((uintptr_t)out + 32) % 4 || co % 4) return BAGUA_ERR_INVALID_ARG;  // bit tiles are written as dwords
+    float* partials = static_cast<float*>(ws);
+    if (tiles > 0)
+        hipLaunchKernelGGL(onebit_encode_kernel<T>, dim3(ob_blocks(tiles, nact), nact), dim3(kBlock), 0, s,
+                           static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, out, co, partials,
+                           tiles);
+    hipLaunchKernelGGL(onebit_finalize_kernel, dim3(nact), dim3(kObFinalizeThreads), 0, s, partials, tiles,
+                       (int64_t)in_num_elem, (int64_t)cs, target, out, co, (int64_t)out_bytes, p);
+    return check_launch();
+}
+
+template <typename T>
+static int ob_decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, hipStream_t s) {
+    using S = typename T::storage;
+    if (p <= 0 || p > 65535 || cs < 0 || !in || !out) return BAGUA_ERR_INVALID_ARG;
+    const int64_t co = (int64_t)(in_bytes / (size_t)p);
+    const int64_t tiles = ob_tiles(cs);
+    if (co < 32 + tiles * kObTileBytes) return BAGUA_ERR_INVALID_ARG;
+    if (((uintptr_t)in + 32) % 4 || co % 4) return BAGUA_ERR_INVALID_ARG;
+    if (tiles == 0) return BAGUA_OK;
+    hipLaunchKernelGGL(onebit_decode_kernel<T>, dim3(ob_blocks(tiles, p), p), dim3(kBlock), 0, s, in, co,
+                       (int64_t)cs, static_cast<S*>(out));
+    return check_launch();
+}
+
+}  // namespace bagua
+
+using namespace bagua;
+
+extern "C" {
+
+size_t bagua_onebit_compressed_bytes(int chunk_size, int num_chunks) {
+    return (size_t)num_chunks * (32 + (size_t)ob_tiles(chunk_size) * kObTileBytes);
+}
+
+size_t bagua_onebit_workspace_bytes(int chunk_size, int num_chunks) {
+    const int64_t t = ob_tiles(chunk_size);
+    return (size_t)(num_chunks > 0 ? num_chunks : 1) * (size_t)(t > 0 ? t : 1) * sizeof(float) + 256;
+}
+
+int bagua_onebit_compress(int dtype, const void* input, int input_num_element, int chunk_size, int num_chunks,
+                          uint8_t* output, size_t output_bytes, void* workspace, size_t workspace_bytes,
+                          int target_chunk, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return ob_compress_impl<F32>(input, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                         workspace, workspace_bytes, target_chunk, s);
+        case BAGUA_DTYPE_F16:
+            return ob_compress_impl<F16>(input, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                         workspace, workspace_bytes, target_chunk, s);
+        case BAGUA_DTYPE_BF16:
+            return ob_compress_impl<BF16>(input, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                          workspace, workspace_bytes, target_chunk, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+int bagua_onebit_decompress(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size, int num_chunks,
+                            void* output, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32: return ob_decompress_impl<F32>(input, input_bytes, chunk_size, num_chunks, output, s);
+        case BAGUA_DTYPE_F16: return ob_decompress_impl<F16>(input, input_bytes, chunk_size, num_chunks, output, s);
+        case BAGUA_DTYPE_BF16: return ob_decompress_impl<BF16>(input, input_bytes, chunk_size, num_chunks, output, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+size_t onebit_temp_size_host(int chunk_size, int num_chunks) {
+    return bagua_onebit_workspace_bytes(chunk_size, num_chunks);
+}
+
+#define V1(call) v1_check((call), __FILE__, __LINE__)
+void compress_f32_to_onebit_host(float* input, int input_num_element, int chunk_size, int num_chunks, uint8_t* output,
+                                 size_t output_size, void* dev_buffer, size_t dev_size, int target_chunk,
+                                 bagua_stream_t stream) {
+    V1(bagua_onebit_compress(BAGUA_DTYPE_F32, input, input_num_element, chunk_size, num_chunks, output, output_size,
+                             dev_buffer, dev_size, target_chunk, stream));
+}
+void compress_bf16_to_onebit_host(bagua_bf16_t* input, int input_num_element, int chunk_size, int num_chunks,
+                                  uint8_t* output, size_t output_size, void* dev_buffer, size_t dev_size,
+                                  int target_chunk, bagua_stream_t stream) {
+    V1(bagua_onebit_compress(BAGUA_DTYPE_BF16, input, input_num_element, chunk_size, num_chunks, output,
+                             output_size, dev_buffer, dev_size, target_chunk, stream));
+}
+void decompress_onebit_to_f32_host(uint8_t* input, size_t input_size, int chunk_size, int num_chunks, float* output,
+                                   bagua_stream_t stream) {
+    V1(bagua_onebit_decompress(BAGUA_DTYPE_F32, input, input_size, chunk_size, num_chunks, output, stream));
+}
+void decompress_onebit_to_bf16_host(uint8_t* input, size_t input_size, int chunk_size, int num_chunks,
+                                    bagua_bf16_t* output, bagua_stream_t stream) {
+    V1(bagua_onebit_decompress(BAGUA_DTYPE_BF16, input, input_size, chunk_size, num_chunks, output, stream));
+}
+#undef V1
+
+}  // extern "C"

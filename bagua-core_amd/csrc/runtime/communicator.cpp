@@ -1,0 +1,274 @@
+// communicator.cpp — RCCL communicator (replaces the Aluminum NCCLBackend
+// wrappers of bagua-core-internal/src/communicators/mod.rs and the C shim
+// bagua-core-c/src/lib.rs:9-69, whose symbols were Rust-mangled: exported
+// unmangled here).
+//
+// One communicator = one ncclComm_t + the stream every collective and codec
+// kernel of the comm ops is enqueued on (the reference binds an
+// Al::NCCLCommunicator to a stream the same way, communicators/mod.rs:44).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <atomic>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "bagua_core.h"
+#include "comm_internal.hpp"
+#include "runtime_util.hpp"
+
+namespace bagua {
+
+static const char kB64[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+
+std::string base64_encode(const uint8_t* p, size_t n) {
+    std::string o;
+    for (size_t i = 0; i < n; i += 3) {
+        uint32_t v = (uint32_t)p[i] << 16;
+        if (i + 1 < n) v |= (uint32_t)p[i + 1] << 8;
+        if (i + 2 < n) v |= p[i + 2];
+        o += kB64[(v >> 18) & 63];
+        o += kB64[(v >> 12) & 63];
+        o += i + 1 < n ? kB64[(v >> 6) & 63] : '=';
+        o += i + 2 < n ? kB64[v & 63] : '=';
+    }
+    return o;
+}
+
+bool base64_decode(const char* s, std::vector<uint8_t>* out) {
+    out->clear();
+    uint32_t v = 0;
+    int bits = 0;
+    for (; *s; ++s) {
+        if (*s == '=') break;
+        const char* f = std::strchr(kB64, *s);
+        if (!f || !*s) return false;
+        v = (v << 6) | (uint32_t)(f - kB64);
+        bits += 6;
+        if (bits >= 8) {
+            bits -= 8;
+            out->push_back((uint8_t)((v >> bits) & 0xff));
+        }
+    }
+    return true;
+}
+
+ncclDataType_t nccl_dtype(int d) {
+    switch (d) {
+        case BAGUA_DTYPE_F32: return ncclFloat32;
+        case BAGUA_DTYPE_F16: return ncclFloat16;
+        case BAGUA_DTYPE_BF16: return ncclBfloat16;
+        case BAGUA_DTYPE_U8: return ncclUint8;
+        case BAGUA_DTYPE_I64: return ncclInt64;
+        case BAGUA_DTYPE_U64: return ncclUint64;
+    }
+    return ncclUint8;
+}
+
+static ncclRedOp_t nccl_op(int op) {
+    switch (op) {
+        case BAGUA_OP_PROD: return ncclProd;
+        case BAGUA_OP_MIN: return ncclMin;
+        case BAGUA_OP_MAX: return ncclMax;
+        case BAGUA_OP_AVG: return ncclAvg;
+    }
+    return ncclSum;
+}
+
+int nccl_status(ncclResult_t r) {
+    if (r == ncclSuccess) return BAGUA_OK;
+    BAGUA_LOG(0, "RCCL error: %s", ncclGetErrorString(r));
+    return BAGUA_ERR_COMM;
+}
+
+}  // namespace bagua
+
+using namespace bagua;
+
+#define COMM_CHECK(c)                                  \
+    do {                                               \
+        if (!(c) || !(c)->comm) return BAGUA_ERR_INVALID_ARG; \
+        if ((c)->aborted.load()) return BAGUA_ERR_ABORTED;    \
+    } while (0)
+
+extern "C" {
+
+int bagua_generate_nccl_unique_id_str(char* buf, size_t buf_len) {
+    // communicators/mod.rs:226-240: base64 of the 128-byte ncclUniqueId
+    ncclUniqueId id;
+    int rc = nccl_status(ncclGetUniqueId(&id));
+    if (rc) return rc;
+    const std::string s = base64_encode(reinterpret_cast<const uint8_t*>(id.internal), NCCL_UNIQUE_ID_BYTES);
+    if (!buf || buf_len < s.size() + 1) return BAGUA_ERR_INVALID_ARG;
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+    return BAGUA_OK;
+}
+
+BaguaSingleCommunicatorC* bagua_single_communicator_c_create(size_t rank, size_t nranks, size_t device_id,
+                                                             uint64_t stream_ptr, const char* nccl_unique_id_str) {
+    // communicators/mod.rs:25-60
+    if (!nccl_unique_id_str || rank >= nranks) return nullptr;
+    if (hipSetDevice((int)device_id) != hipSuccess) return nullptr;
+    std::vector<uint8_t> bytes;
+    if (!base64_decode(nccl_unique_id_str, &bytes) || bytes.size() < NCCL_UNIQUE_ID_BYTES) return nullptr;
+    ncclUniqueId id;
+    std::memcpy(id.internal, bytes.data(), NCCL_UNIQUE_ID_BYTES);
+    auto* c = new BaguaSingleCommunicatorC();
+    c->rank = rank;
+    c->nranks = nranks;
+    c->device_id = (int)device_id;
+    c->stream = (hipStream_t)(uintptr_t)stream_ptr;
+    if (ncclCommInitRank(&c->comm, (int)nranks, id, (int)rank) != ncclSuccess) {
+        delete c;
+        return nullptr;
+    }
+    BAGUA_LOG(3, "communicator rank %zu/%zu on device %zu ready", rank, nranks, device_id);
+    return c;
+}
+
+void bagua_single_communicator_c_destroy(BaguaSingleCommunicatorC** ptr) {
+    // bagua-core-c/src/lib.rs:32-53: null-safe, nulls the caller's pointer
+    if (!ptr || !*ptr) return;
+    BaguaSingleCommunicatorC* c = *ptr;
+    if (c->comm) {
+        if (c->aborted.load()) (void)ncclCommAbort(c->comm);
+        else (void)ncclCommDestroy(c->comm);
+    }
+    delete c;
+    *ptr = nullptr;
+}
+
+int32_t bagua_single_communicator_c_nranks(BaguaSingleCommunicatorC** ptr, size_t* nranks) {
+    // bagua-core-c/src/lib.rs:55-69: 0 success, -1 null pointer
+    if (!ptr || !*ptr || !nranks) return -1;
+    *nranks = (*ptr)->nranks;
+    return 0;
+}
+
+int32_t bagua_single_communicator_c_rank(BaguaSingleCommunicatorC** ptr, size_t* rank) {
+    if (!ptr || !*ptr || !rank) return -1;
+    *rank = (*ptr)->rank;
+    return 0;
+}
+
+uint64_t bagua_single_communicator_c_stream(BaguaSingleCommunicatorC* c) {
+    return c ? (uint64_t)(uintptr_t)c->stream : 0;
+}
+
+int bagua_comm_abort(BaguaSingleCommunicatorC* c) {
+    // communicators/mod.rs:456-466
+    if (!c) return BAGUA_ERR_INVALID_ARG;
+    c->aborted.store(true);
+    int rc = BAGUA_OK;
+    if (c->comm) {
+        rc = nccl_status(ncclCommAbort(c->comm));
+        c->comm = nullptr;
+    }
+    return rc;
+}
+
+int bagua_comm_check_abort(BaguaSingleCommunicatorC* c) { return c && c->aborted.load() ? 1 : 0; }
+
+int bagua_comm_allreduce_inplace(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int op) {
+    // communicators/mod.rs:1020-1043 (count = num_elements_allocated)
+    COMM_CHECK(c);
+    if (!t) return BAGUA_ERR_INVALID_ARG;
+    void* p = (void*)(uintptr_t)t->ptr;
+    return nccl_status(ncclAllReduce(p, p, t->num_elem_allocated, nccl_dtype(t->dtype), nccl_op(op), c->comm, c->stream));
+}
+
+int bagua_comm_allreduce(BaguaSingleCommunicatorC* c, const bagua_tensor_t* s, const bagua_tensor_t* r, int op) {
+    COMM_CHECK(c);
+    if (!s || !r || s->dtype != r->dtype || s->num_elem_allocated != r->num_elem_allocated) return BAGUA_ERR_INVALID_ARG;
+    return nccl_status(ncclAllReduce((const void*)(uintptr_t)s->ptr, (void*)(uintptr_t)r->ptr, s->num_elem_allocated,
+                                     nccl_dtype(s->dtype), nccl_op(op), c->comm, c->stream));
+}
+
+int bagua_comm_broadcast(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int root) {
+    COMM_CHECK(c);
+    if (!t) return BAGUA_ERR_INVALID_ARG;
+    void* p = (void*)(uintptr_t)t->ptr;
+    return nccl_status(ncclBroadcast(p, p, t->num_elem_allocated, nccl_dtype(t->dtype), root, c->comm, c->stream));
+}
+
+int bagua_comm_alltoall(BaguaSingleCommunicatorC* c, const bagua_tensor_t* s, const bagua_tensor_t* r) {
+    COMM_CHECK(c);
+    if (!s || !r || s->dtype != r->dtype || s->num_elem_allocated % c->nranks ||
+        r->num_elem_allocated < s->num_elem_allocated)
+        return BAGUA_ERR_INVALID_ARG;
+    const size_t count = s->num_elem_allocated / c->nranks;
+    return nccl_status(ncclAllToAll((const void*)(uintptr_t)s->ptr, (void*)(uintptr_t)r->ptr, count,
+                                    nccl_dtype(s->dtype), c->comm, c->stream));
+}
+
+int bagua_comm_alltoall_inplace(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t) {
+    // communicators/mod.rs:602-630: count = allocated / nranks; rank r's slot r*count
+    COMM_CHECK(c);
+    if (!t || t->num_elem_allocated % c->nranks) return BAGUA_ERR_INVALID_ARG;  // "tensors must be aligned"
+    const size_t bytes = t->num_elem_allocated * bagua_dtype_bytes(t->dtype);
+    PoolBuffer tmp;
+    int rc = tmp.allocate(c->device_id, bytes);
+    if (rc) return rc;
+    bagua_tensor_t r = *t;
+    r.ptr = tmp.ptr();
+    rc = bagua_comm_alltoall(c, t, &r);
+    if (rc) return rc;
+    if (hipMemcpyAsync((void*)(uintptr_t)t->ptr, tmp.as<void>(), bytes, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+        return BAGUA_ERR_HIP;
+    // the temp block goes back to the pool only after the copy has drained
+    return hipStreamSynchronize(c->stream) == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP;
+}
+
+int bagua_comm_allgather_inplace(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t) {
+    // communicators/mod.rs:760-787: in-place allgather, own slot at rank*count
+    COMM_CHECK(c);
+    if (!t || t->num_elem_allocated % c->nranks) return BAGUA_ERR_INVALID_ARG;
+    const size_t count = t->num_elem_allocated / c->nranks;
+    uint8_t* base = (uint8_t*)(uintptr_t)t->ptr;
+    const size_t esz = bagua_dtype_bytes(t->dtype);
+    return nccl_status(ncclAllGather(base + c->rank * count * esz, base, count, nccl_dtype(t->dtype), c->comm, c->stream));
+}
+
+int bagua_comm_allgather(BaguaSingleCommunicatorC* c, const bagua_tensor_t* s, const bagua_tensor_t* r) {
+    COMM_CHECK(c);
+    if (!s || !r || r->num_elem_allocated != s->num_elem_allocated * c->nranks) return BAGUA_ERR_INVALID_ARG;
+    return nccl_status(ncclAllGather((const void*)(uintptr_t)s->ptr, (void*)(uintptr_t)r->ptr, s->num_elem_allocated,
+                                     nccl_dtype(s->dtype), c->comm, c->stream));
+}
+
+int bagua_comm_send(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int peer) {
+    COMM_CHECK(c);
+    if (!t) return BAGUA_ERR_INVALID_ARG;
+    return nccl_status(ncclSend((const void*)(uintptr_t)t->ptr, t->num_elem_allocated, nccl_dtype(t->dtype), peer,
+                                c->comm, c->stream));
+}
+
+int bagua_comm_recv(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int peer) {
+    COMM_CHECK(c);
+    if (!t) return BAGUA_ERR_INVALID_ARG;
+    return nccl_status(ncclRecv((void*)(uintptr_t)t->ptr, t->num_elem_allocated, nccl_dtype(t->dtype), peer, c->comm,
+                                c->stream));
+}
+
+int bagua_comm_group_start(void) { return nccl_status(ncclGroupStart()); }
+int bagua_comm_group_end(void) { return nccl_status(ncclGroupEnd()); }
+
+int bagua_comm_synchronize(BaguaSingleCommunicatorC* c) {
+    if (!c) return BAGUA_ERR_INVALID_ARG;
+    return hipStreamSynchronize(c->stream) == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP;
+}
+
+int bagua_comm_barrier(BaguaSingleCommunicatorC* c) {
+    // communicators/mod.rs:973-: a tiny allreduce, then wait for it
+    COMM_CHECK(c);
+    PoolBuffer b;
+    int rc = b.allocate(c->device_id, 4);
+    if (rc) return rc;
+    if (hipMemsetAsync(b.as<void>(), 0, 4, c->stream) != hipSuccess) return BAGUA_ERR_HIP;
+    rc = nccl_status(ncclAllReduce(b.as<void>(), b.as<void>(), 1, ncclFloat32, ncclSum, c->comm, c->stream));
+    if (rc) return rc;
+    return bagua_comm_synchronize(c);
+}
+
+}  // extern "C"

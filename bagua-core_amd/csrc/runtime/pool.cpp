@@ -1,0 +1,138 @@
+// pool.cpp — device memory pool (replaces CUDA_DEVICE_MEMORY_POOL,
+// bagua-core-internal/src/resource_pool/mod.rs:11-60: a sized object pool of
+// cudaMalloc'd blocks per device).
+//
+// Size classes are 4 per power of two (<= 25 % slack), so a 1 GiB gradient
+// bucket and its ~256 MiB compressed buffer do not double in size the way a
+// power-of-two pool would on a 288 GB HBM device.  Blocks are reused per
+// class; bagua_pool_trim() returns cached blocks to HIP.
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "bagua_core.h"
+#include "runtime_util.hpp"
+
+namespace bagua {
+namespace {
+
+size_t size_class(size_t bytes) {
+    if (bytes <= 256) return 256;
+    size_t p = 1;
+    while (p < bytes) p <<= 1;  // p/2 < bytes <= p
+    const size_t q = p / 8;     // quarter steps between p/2 and p
+    size_t c = p / 2;
+    while (c < bytes) c += q;
+    return c;
+}
+
+struct DevicePool {
+    std::map<size_t, std::vector<uint64_t>> free_blocks;  // class -> blocks
+    size_t in_use = 0, cached = 0;
+};
+
+struct Pool {
+    std::mutex mu;
+    std::unordered_map<int, DevicePool> dev;
+    std::unordered_map<uint64_t, std::pair<int, size_t>> live;  // ptr -> (device, class)
+};
+
+Pool& pool() {
+    static Pool* p = new Pool();  // never destroyed: blocks may outlive static teardown
+    return *p;
+}
+
+}  // namespace
+
+int pool_alloc(int device_id, size_t bytes, uint64_t* out) {
+    if (!out) return BAGUA_ERR_INVALID_ARG;
+    const size_t cls = size_class(bytes ? bytes : 1);
+    Pool& P = pool();
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        DevicePool& d = P.dev[device_id];
+        auto it = d.free_blocks.find(cls);
+        if (it != d.free_blocks.end() && !it->second.empty()) {
+            *out = it->second.back();
+            it->second.pop_back();
+            d.cached -= cls;
+            d.in_use += cls;
+            P.live[*out] = {device_id, cls};
+            return BAGUA_OK;
+        }
+    }
+    DeviceGuard guard(device_id);
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, cls);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        // free cached blocks of this device and retry once
+        pool_trim(device_id);
+        e = hipMalloc(&p, cls);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return BAGUA_ERR_OOM;
+        }
+    }
+    std::lock_guard<std::mutex> g(P.mu);
+    *out = (uint64_t)(uintptr_t)p;
+    P.dev[device_id].in_use += cls;
+    P.live[*out] = {device_id, cls};
+    return BAGUA_OK;
+}
+
+int pool_free(uint64_t ptr) {
+    if (!ptr) return BAGUA_OK;
+    Pool& P = pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.live.find(ptr);
+    if (it == P.live.end()) return BAGUA_ERR_INVALID_ARG;
+    const int dev = it->second.first;
+    const size_t cls = it->second.second;
+    P.live.erase(it);
+    DevicePool& d = P.dev[dev];
+    d.in_use -= cls;
+    d.cached += cls;
+    d.free_blocks[cls].push_back(ptr);
+    return BAGUA_OK;
+}
+
+int pool_trim(int device_id) {
+    Pool& P = pool();
+    std::vector<uint64_t> release;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        DevicePool& d = P.dev[device_id];
+        for (auto& kv : d.free_blocks) {
+            for (uint64_t p : kv.second) release.push_back(p);
+            kv.second.clear();
+        }
+        d.cached = 0;
+    }
+    if (release.empty()) return BAGUA_OK;
+    DeviceGuard guard(device_id);
+    (void)hipDeviceSynchronize();  // a cached block may still be read by queued work
+    for (uint64_t p : release) (void)hipFree((void*)(uintptr_t)p);
+    return BAGUA_OK;
+}
+
+size_t pool_bytes(int device_id, bool cached) {
+    Pool& P = pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.dev.find(device_id);
+    if (it == P.dev.end()) return 0;
+    return cached ? it->second.cached : it->second.in_use;
+}
+
+}  // namespace bagua
+
+extern "C" {
+int bagua_pool_alloc(int device_id, size_t bytes, uint64_t* ptr) { return bagua::pool_alloc(device_id, bytes, ptr); }
+int bagua_pool_free(uint64_t ptr) { return bagua::pool_free(ptr); }
+int bagua_pool_trim(int device_id) { return bagua::pool_trim(device_id); }
+size_t bagua_pool_bytes_in_use(int device_id) { return bagua::pool_bytes(device_id, false); }
+size_t bagua_pool_bytes_cached(int device_id) { return bagua::pool_bytes(device_id, true); }
+}

@@ -1,0 +1,82 @@
+// runtime_util.hpp — internal helpers of the host runtime.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "bagua_core.h"
+
+namespace bagua {
+
+int pool_alloc(int device_id, size_t bytes, uint64_t* out);
+int pool_free(uint64_t ptr);
+int pool_trim(int device_id);
+size_t pool_bytes(int device_id, bool cached);
+
+// Per-(device, stream) scratch reused by every launch on that stream; stream
+// order makes reuse safe without host synchronisation.
+uint64_t stream_workspace(int device_id, uint64_t stream, size_t bytes);
+
+// RAII current-device switch (communicators/mod.rs:32-35 does cudaSetDevice)
+class DeviceGuard {
+   public:
+    explicit DeviceGuard(int device) {
+        (void)hipGetDevice(&prev_);
+        if (device >= 0 && device != prev_) {
+            (void)hipSetDevice(device);
+            switched_ = true;
+        }
+    }
+    ~DeviceGuard() {
+        if (switched_) (void)hipSetDevice(prev_);
+    }
+
+   private:
+    int prev_ = 0;
+    bool switched_ = false;
+};
+
+// RAII pool allocation
+class PoolBuffer {
+   public:
+    PoolBuffer() = default;
+    PoolBuffer(const PoolBuffer&) = delete;
+    PoolBuffer& operator=(const PoolBuffer&) = delete;
+    ~PoolBuffer() { reset(); }
+    int allocate(int device, size_t bytes) {
+        reset();
+        bytes_ = bytes;
+        return pool_alloc(device, bytes, &ptr_);
+    }
+    void reset() {
+        if (ptr_) pool_free(ptr_);
+        ptr_ = 0;
+    }
+    uint64_t ptr() const { return ptr_; }
+    size_t bytes() const { return bytes_; }
+    template <typename P>
+    P* as() const { return reinterpret_cast<P*>((uintptr_t)ptr_); }
+
+   private:
+    uint64_t ptr_ = 0;
+    size_t bytes_ = 0;
+};
+
+// level-filtered stderr logging (the reference's LOG_LEVEL env, py/lib.rs:489-496)
+int log_level();  // 0=error 1=warn 2=info 3=debug
+#define BAGUA_LOG(level, ...)                                   \
+    do {                                                        \
+        if (::bagua::log_level() >= (level)) {                  \
+            std::fprintf(stderr, "[bagua-core] " __VA_ARGS__);  \
+            std::fputc('\n', stderr);                           \
+        }                                                       \
+    } while (0)
+
+inline bool is_float_dtype(int d) {
+    return d == BAGUA_DTYPE_F32 || d == BAGUA_DTYPE_F16 || d == BAGUA_DTYPE_BF16;
+}
+
+}  // namespace bagua

@@ -1,0 +1,311 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X bagua-core gradient codec.
+
+Metric (BASELINE.json): "GiB/s fp32 gradient encode+decode (device-resident);
+1/2/4/8-GPU compressed all-reduce GiB/s".
+
+  N = 1 (default): config 2 — one 256 MiB fp32 bucket (2^26 elements,
+      n_chunks = 1), one step = MinMax-UInt8 encode (min/max pass + quantise
+      pass) + decode, inputs resident in HBM.  value = 4*2^26 B / step time.
+  N > 1 (torchrun, one rank per GPU): config 4 — every rank owns a 1 GiB fp32
+      gradient (2^28 elements, seed 0x5EED + rank); one step = the compressed
+      centralized all-reduce (compress -> RCCL alltoall -> fused dequantise +
+      reduce + requantise -> RCCL allgather -> decompress).  value = the
+      gradient bytes all ranks reduced / max-over-ranks step time (weak scaling:
+      per-GPU bucket fixed).  The uncompressed fp32 RCCL all-reduce of the same
+      bucket is timed beside it (fp32_allreduce_gib_s, ratio_vs_fp32).
+
+Every byte is produced by the gfx950 kernels through the C ABI
+(bagua-core_amd/lib/*.so).  The oracle is used ONLY for the cpu_baseline leg
+(rank 0, N = 1): the C restatement of the reference kernels timed on the
+host's cores on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "bagua-core_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+METRIC = ("GiB/s fp32 gradient encode+decode (device-resident); "
+          "1/2/4/8-GPU compressed all-reduce GiB/s")
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+GiB = float(1 << 30)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=["auto", "codec", "allreduce", "onebit"], default="auto")
+    ap.add_argument("--elements", type=int, default=0, help="override bucket elements")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=4.0, help="wall budget of the cpu_baseline leg")
+    return ap.parse_args()
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
+    summary (profiles/r01_pmc_traffic.json, produced by
+    profiles/collect_pmc.py following MI355X_MICROARCH.md §HBM: FETCH_SIZE
+    doubled for 16-B streaming reads, WRITE_SIZE as is), or None."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+        return d.get("per_launch_hbm_bytes", {}).get(kernel)
+    except (OSError, ValueError):
+        return None
+
+
+# ----------------------------------------------------------------- N = 1 ------
+def bench_codec(args, onebit: bool = False):
+    from bagua_core import _native as N
+    K = N.K
+    n = args.elements or (1 << 26)
+    p = 1
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    g = torch.Generator(device=dev).manual_seed(0x5EED)
+    x = torch.randn(n, device=dev, generator=g) * 1e-3
+    y = torch.empty_like(x)
+    stream = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    if onebit:
+        S = K.bagua_onebit_compressed_bytes(n, p)
+        ws_bytes = K.bagua_onebit_workspace_bytes(n, p)
+    else:
+        S = K.bagua_minmax_u8_compressed_bytes(0, n, p)
+        ws_bytes = K.bagua_minmax_u8_workspace_bytes(n, p)
+    comp = torch.empty(S, dtype=torch.uint8, device=dev)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    xp, yp, cp, wp = x.data_ptr(), y.data_ptr(), comp.data_ptr(), ws.data_ptr()
+
+    if onebit:
+        names = ["onebit_encode+finalize", "onebit_decode"]
+
+        def launches():
+            return [lambda: K.bagua_onebit_compress(0, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
+                    lambda: K.bagua_onebit_decompress(0, cp, S, n, p, yp, sp)]
+        alg = [4 * n + n // 8 + 32, n // 8 + 32 + 4 * n]
+    else:
+        names = ["minmax_partials_kernel", "minmax_quantize_kernel", "minmax_dequantize_kernel"]
+
+        def launches():
+            return [lambda: K.bagua_minmax_u8_compress_stage(1, 0, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
+                    lambda: K.bagua_minmax_u8_compress_stage(2, 0, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
+                    lambda: K.bagua_minmax_u8_decompress(0, cp, S, n, p, yp, sp)]
+        # algorithmic bytes per launch: partials read 4N; quantise read 4N + write N + header;
+        # dequantise read N + header, write 4N.  Sum = 14N + 64p.
+        alg = [4 * n, 4 * n + n + 32, n + 32 + 4 * n]
+    calls = launches()
+
+    def step():
+        for c in calls:
+            rc = c()
+            if rc:
+                raise RuntimeError(f"kernel launch failed: {N.STATUS.get(rc, rc)}")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # timed region: K steps, per-launch HIP events on the launch stream
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(calls) + 1)] for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        for i, c in enumerate(calls):
+            rc = c()
+            if rc:
+                raise RuntimeError(f"kernel launch failed: {N.STATUS.get(rc, rc)}")
+            ev[k][i + 1].record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    per = [sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(args.steps)) / args.steps for i in range(len(calls))]
+    ms = wall * 1e3 / args.steps
+    value = 4.0 * n / (ms * 1e-3) / GiB
+    dom = max(range(len(calls)), key=lambda i: per[i])
+    achieved = alg[dom] / (per[dom] * 1e-3) / 1e9
+    step_alg = sum(alg)
+    traffic = pmc_traffic(names[dom])
+    roof = {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "alg_bytes_per_launch": alg[dom], "avg_launch_us": round(per[dom] * 1e3, 2)}
+    extra = {
+        "per_kernel_us": {nm: round(t * 1e3, 2) for nm, t in zip(names, per)},
+        "per_kernel_gbs": {nm: round(a / (t * 1e-3) / 1e9, 1) for nm, a, t in zip(names, alg, per)},
+        "step_roofline": {"alg_bytes": step_alg, "event_us": round(sum(per) * 1e3, 2),
+                          "achieved_gbs": round(step_alg / (sum(per) * 1e-3) / 1e9, 1),
+                          "frac": round(step_alg / (sum(per) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "encode_gib_s": round(4.0 * n / (sum(per[:-1]) * 1e-3) / GiB, 1),
+        "decode_gib_s": round(4.0 * n / (per[-1] * 1e-3) / GiB, 1),
+    }
+    cfg = {"workload": ("onebit_sign_scale" if onebit else "minmax_uint8") +
+           f"_encode_decode_{4 * n >> 20}MiB_fp32_bucket", "bucket_elements": n, "n_chunks": p,
+           "compressed_bytes": S, "config_index": 3 if onebit else 2}
+    return value, ms, roof, cfg, extra, x
+
+
+def cpu_baseline(args, sample_elems: int = 1 << 24):
+    """The reference's algorithm (C restatement, oracle/bagua_oracle.c) on the
+    host cores: encode+decode of a bounded sample of the same workload."""
+    import numpy as np
+    from oracle import oracle_c
+    lib_threads = oracle_c.num_threads()
+    rng = np.random.default_rng(0x5EED)
+    x = (rng.standard_normal(sample_elems) * 1e-3).astype(np.float32)
+    out = np.empty_like(x)
+    buf = oracle_c.compress_minmax_u8(x, 0, 1)
+    oracle_c.decompress_minmax_u8(buf, 1, out, 0)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        oracle_c.compress_minmax_u8(x, 0, 1, out=buf)
+        oracle_c.decompress_minmax_u8(buf, 1, out, 0)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or reps >= 200:
+            break
+    return {"value": round(4.0 * sample_elems * reps / el / GiB, 3), "unit": "GiB/s", "cores": lib_threads,
+            "kind": "port",
+            "sample": f"{4 * sample_elems >> 20} MiB fp32 N(0,1e-3^2) bucket, MinMax-UInt8 encode+decode x{reps} "
+                      f"({el:.1f} s wall, {lib_threads} OpenMP threads, oracle/bagua_oracle.c)"}
+
+
+# ----------------------------------------------------------------- N > 1 ------
+def bench_allreduce(args, world: int, rank: int, local_rank: int):
+    import torch.distributed as dist
+    from bagua_core import BaguaSingleCommunicatorPy, BaguaTensorPy
+    from bagua_core import _native as N
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    uid = [BaguaSingleCommunicatorPy.generate_nccl_unique_id_str() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0)
+    comm_stream = torch.cuda.Stream(device=dev)
+    comm = BaguaSingleCommunicatorPy(rank, world, local_rank, comm_stream.cuda_stream, uid[0])
+    n = args.elements or (1 << 28)
+    n -= n % world
+    g = torch.Generator(device=dev).manual_seed(0x5EED + rank)
+    x = torch.randn(n, device=dev, generator=g) * 1e-3
+    torch.cuda.synchronize()
+    raw = BaguaTensorPy(x, "gradient_bucket").raw()
+
+    def compressed_step():
+        N.check(N.C.bagua_centralized_low_precision_synchronous(comm.handle, ctypes.byref(raw), 1,
+                                                                N.COMPRESSION_MINMAX_UINT8), "compressed allreduce")
+
+    def fp32_step():
+        N.check(N.C.bagua_centralized_full_precision_synchronous(comm.handle, ctypes.byref(raw), 1), "fp32 allreduce")
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def timed(fn, steps, warm):
+        for _ in range(warm):
+            fn()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()) / steps
+
+    t_c = timed(compressed_step, args.steps, args.warmup)
+    t_f = timed(fp32_step, max(3, args.steps // 2), max(1, args.warmup // 2))
+    value = world * 4.0 * n / t_c / GiB
+    per_rank = 4.0 * n / t_c / GiB
+    fp32 = 4.0 * n / t_f / GiB
+    # roofline of the dominant codec kernel on this bucket (p = world chunks), HIP events on its stream
+    K = N.K
+    S = K.bagua_minmax_u8_compressed_bytes(0, n // world, world)
+    comp = torch.empty(S, dtype=torch.uint8, device=dev)
+    wsb = K.bagua_minmax_u8_workspace_bytes(n // world, world)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(st.cuda_stream)
+    y = torch.empty_like(x)
+    calls = [lambda: K.bagua_minmax_u8_compress_stage(1, 0, x.data_ptr(), n, n // world, world, comp.data_ptr(), S,
+                                                       ws.data_ptr(), wsb, -1, sp),
+             lambda: K.bagua_minmax_u8_compress_stage(2, 0, x.data_ptr(), n, n // world, world, comp.data_ptr(), S,
+                                                       ws.data_ptr(), wsb, -1, sp),
+             lambda: K.bagua_minmax_u8_decompress(0, comp.data_ptr(), S, n // world, world, y.data_ptr(), sp)]
+    names = ["minmax_partials_kernel", "minmax_quantize_kernel", "minmax_dequantize_kernel"]
+    alg = [4 * n, 5 * n + 32 * world, 5 * n + 32 * world]
+    reps = 5
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(reps)]
+    for c in calls:
+        c()
+    for k in range(reps):
+        ev[k][0].record(st)
+        for i, c in enumerate(calls):
+            c()
+            ev[k][i + 1].record(st)
+    torch.cuda.synchronize()
+    per = [sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(reps)) / reps for i in range(3)]
+    dom = max(range(3), key=lambda i: per[i])
+    achieved = alg[dom] / (per[dom] * 1e-3) / 1e9
+    roof = {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(names[dom]),
+            "alg_bytes_per_launch": alg[dom], "avg_launch_us": round(per[dom] * 1e3, 2)}
+    cfg = {"workload": f"minmax_uint8_compressed_allreduce_{4 * n >> 20}MiB_fp32_per_rank", "bucket_elements": n,
+           "n_chunks": world, "collectives": "rccl alltoall + allgather (uint8)", "parallelism": f"dp{world}",
+           "config_index": 4}
+    extra = {"per_rank_gib_s": round(per_rank, 2), "fp32_allreduce_gib_s": round(fp32, 2),
+             "ratio_vs_fp32": round(per_rank / fp32, 3), "fp32_ms_per_step": round(t_f * 1e3, 3),
+             "per_kernel_us": {nm: round(t * 1e3, 2) for nm, t in zip(names, per)}}
+    del comm
+    return value, t_c * 1e3, roof, cfg, extra
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", args.gpus))
+    rank = int(os.environ.get("RANK", 0))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    workload = args.workload
+    if workload == "auto":
+        workload = "codec" if world == 1 else "allreduce"
+    cpu = None
+    if workload in ("codec", "onebit"):
+        value, ms, roof, cfg, extra, _ = bench_codec(args, onebit=(workload == "onebit"))
+        if rank == 0 and world == 1 and not args.no_cpu_baseline and workload == "codec":
+            cpu = cpu_baseline(args)
+        dtype = "f32 -> u8" if workload == "codec" else "f32 -> 1bit"
+    else:
+        value, ms, roof, cfg, extra = bench_allreduce(args, world, rank, local_rank)
+        dtype = "f32 -> u8"
+    if rank == 0:
+        line = {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": dtype,
+                "data": "synthetic fp32 gradients N(0, 1e-3^2) (torch.randn, seed 0x5EED + rank), resident in HBM",
+                "config": cfg, "roofline": roof, "cpu_baseline": cpu}
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.barrier()
+            dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

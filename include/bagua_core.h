@@ -1,0 +1,135 @@
+/*
+ * bagua_core.h — C ABI of the MI355X host runtime (libbagua_core.so).
+ *
+ * Replaces, behind plain pointers and sizes, the parts of the reference's
+ * Rust host that sit on the compressed-gradient path:
+ *   - device memory pool      bagua-core-internal/src/resource_pool/mod.rs:11-60
+ *   - tensor codec dispatch   bagua-core-internal/src/datatypes/mod.rs:313-484,665-742
+ *   - communicator            bagua-core-internal/src/communicators/mod.rs:25-60,430-1043
+ *                             bagua-core-c/src/lib.rs:9-69 (C shim, exported UNMANGLED here)
+ *   - comm ops                src/comm_ops/centralized_low_precision_synchronous.rs:16-73
+ *                             src/comm_ops/decentralized_low_precision_synchronous.rs:23-154
+ * Collectives are RCCL (librccl) over xGMI; no Aluminum, no MPI.
+ *
+ * Every function returns a bagua_status_t-compatible int (0 = ok) unless it
+ * returns a size or handle; nothing here calls exit().
+ */
+#ifndef BAGUA_CORE_H
+#define BAGUA_CORE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "bagua_kernels.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* tensor dtypes: kernels' F32/F16/BF16 plus the reference's U8/I64/U64 (datatypes/mod.rs:40-47) */
+enum { BAGUA_DTYPE_U8 = 3, BAGUA_DTYPE_I64 = 4, BAGUA_DTYPE_U64 = 5 };
+
+/* compression methods: "MinMaxUInt8" (datatypes/mod.rs:744-747) and the 1-bit extension */
+enum { BAGUA_COMPRESSION_NONE = 0, BAGUA_COMPRESSION_MINMAX_UINT8 = 1, BAGUA_COMPRESSION_ONEBIT = 2 };
+
+/* reduction ops, Aluminum/BaguaReductionOp numbering (datatypes/mod.rs:24-38) */
+enum { BAGUA_OP_SUM = 0, BAGUA_OP_PROD = 1, BAGUA_OP_MIN = 2, BAGUA_OP_MAX = 3, BAGUA_OP_AVG = 10 };
+
+enum { BAGUA_ERR_COMM = 16, BAGUA_ERR_OOM = 17, BAGUA_ERR_ABORTED = 18 };
+
+/* BaguaTensorRaw (datatypes/mod.rs:79-86) without the Rust ownership vector */
+typedef struct bagua_tensor {
+    uint64_t ptr;
+    uint64_t num_elem;
+    uint64_t num_elem_allocated;
+    int32_t dtype;
+    int32_t device_id;
+} bagua_tensor_t;
+
+size_t bagua_dtype_bytes(int dtype);
+/* cuda_utils.rs:1-6: synchronous device-to-host copy (to_numpy_* read-back) */
+int bagua_memcpy_device_to_host_sync(void* host, uint64_t device_ptr, size_t bytes);
+/* datatypes/mod.rs:969-980: make `stream` wait for a tensor's ready event (0 = no event) */
+int bagua_stream_wait_event(uint64_t stream, uint64_t event);
+
+/* ---------------------------------------------------------------- pool -- */
+/* CUDA_DEVICE_MEMORY_POOL (resource_pool/mod.rs:53-60): size-classed reuse of hipMalloc'd blocks */
+int bagua_pool_alloc(int device_id, size_t bytes, uint64_t* ptr);
+int bagua_pool_free(uint64_t ptr);
+int bagua_pool_trim(int device_id);
+size_t bagua_pool_bytes_in_use(int device_id);
+size_t bagua_pool_bytes_cached(int device_id);
+
+/* --------------------------------------------------------- tensor codec -- */
+/* MinMaxUInt8CompressionParameters::get_compressed_buffer_size (datatypes/mod.rs:669-704) */
+size_t bagua_compressed_size(int method, int dtype, size_t n_chunks, size_t chunk_size);
+/* RawBaguaTensor::compress (datatypes/mod.rs:313-396): `out` receives a pool-owned U8
+ * tensor of bagua_compressed_size() bytes (release it with bagua_pool_free). */
+int bagua_tensor_compress(const bagua_tensor_t* t, int method, int n_chunks, uint64_t stream,
+                          int target_chunk, bagua_tensor_t* out);
+/* the same into a caller-provided U8 buffer of exactly bagua_compressed_size() bytes */
+int bagua_tensor_compress_into(const bagua_tensor_t* t, int method, int n_chunks, uint64_t stream,
+                               int target_chunk, const bagua_tensor_t* out);
+/* RawBaguaTensor::decompress_from (datatypes/mod.rs:398-446) */
+int bagua_tensor_decompress_from(const bagua_tensor_t* t, int method, int n_chunks,
+                                 const bagua_tensor_t* compressed, uint64_t stream);
+/* reduce_mean_inplace / reduce_sum_inplace (datatypes/mod.rs:448-522) */
+int bagua_tensor_reduce_inplace(const bagua_tensor_t* t, int n_chunks, int target_chunk, int average,
+                                uint64_t stream);
+/* add / addmul / clone_from (datatypes/mod.rs:129-274) */
+int bagua_tensor_add_inplace(const bagua_tensor_t* t, const bagua_tensor_t* other, uint64_t stream);
+int bagua_tensor_addmul_inplace(const bagua_tensor_t* t, const bagua_tensor_t* other, float factor,
+                                uint64_t stream);
+int bagua_tensor_clone_from(const bagua_tensor_t* t, const bagua_tensor_t* other, uint64_t stream);
+
+/* --------------------------------------------------------- communicator -- */
+typedef struct BaguaSingleCommunicatorC BaguaSingleCommunicatorC;
+
+/* bagua-core-c/src/lib.rs:9-69, unmangled; nccl_unique_id_str is base64 of ncclUniqueId */
+BaguaSingleCommunicatorC* bagua_single_communicator_c_create(size_t rank, size_t nranks, size_t device_id,
+                                                             uint64_t stream_ptr,
+                                                             const char* nccl_unique_id_str);
+void bagua_single_communicator_c_destroy(BaguaSingleCommunicatorC** ptr);
+int32_t bagua_single_communicator_c_nranks(BaguaSingleCommunicatorC** ptr, size_t* nranks);
+/* additional accessors / collectives (communicators/mod.rs) */
+int32_t bagua_single_communicator_c_rank(BaguaSingleCommunicatorC** ptr, size_t* rank);
+uint64_t bagua_single_communicator_c_stream(BaguaSingleCommunicatorC* comm);
+int bagua_generate_nccl_unique_id_str(char* buf, size_t buf_len);
+int bagua_comm_abort(BaguaSingleCommunicatorC* comm);
+int bagua_comm_check_abort(BaguaSingleCommunicatorC* comm);
+int bagua_comm_allreduce_inplace(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t, int op);
+int bagua_comm_allreduce(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* send, const bagua_tensor_t* recv,
+                         int op);
+int bagua_comm_broadcast(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t, int root);
+int bagua_comm_alltoall(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* send, const bagua_tensor_t* recv);
+int bagua_comm_alltoall_inplace(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t);
+int bagua_comm_allgather_inplace(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t);
+int bagua_comm_allgather(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* send, const bagua_tensor_t* recv);
+int bagua_comm_send(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t, int peer);
+int bagua_comm_recv(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t, int peer);
+int bagua_comm_group_start(void);
+int bagua_comm_group_end(void);
+int bagua_comm_barrier(BaguaSingleCommunicatorC* comm);
+int bagua_comm_synchronize(BaguaSingleCommunicatorC* comm);
+
+/* ------------------------------------------------------------- comm ops -- */
+/* CentralizedLowPrecisionSynchronous::execute_background_communication on one
+ * flat communication tensor (centralized_low_precision_synchronous.rs:16-73). */
+int bagua_centralized_low_precision_synchronous(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,
+                                                int average, int method);
+/* the reference's unfused sequence, kept for A/B measurement and parity */
+int bagua_centralized_low_precision_synchronous_unfused(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,
+                                                        int average, int method);
+/* CentralizedFullPrecisionSynchronous (allreduce SUM/AVG), the baseline denominator */
+int bagua_centralized_full_precision_synchronous(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,
+                                                 int average);
+/* DecentralizedLowPrecisionSynchronous, ring peers (decentralized_low_precision_synchronous.rs:23-154) */
+int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,
+                                                  const bagua_tensor_t* weight,
+                                                  const bagua_tensor_t* left_peer_weight,
+                                                  const bagua_tensor_t* right_peer_weight, int method);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BAGUA_CORE_H */

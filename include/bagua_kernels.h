@@ -1,0 +1,195 @@
+/*
+ * bagua_kernels.h — C ABI of the MI355X (gfx950) gradient-codec kernels.
+ *
+ * Drop-in replacement for the `extern "C"` block of the reference
+ * (bagua-core-internal/kernels/bagua_kernels.cu:573-691), which the Rust host
+ * binds in bagua-core-internal/src/kernels/mod.rs:3-137 with
+ * `#[link(name = "bagua_kernels", kind = "static")]`.  Built as
+ * libbagua_kernels.so / libbagua_kernels.a from bagua-core_amd/csrc/kernels.
+ *
+ * Streams are opaque pointers (`hipStream_t`, ABI-identical to the
+ * reference's `cudaStream_t`; 0 = the null stream).  All calls are
+ * asynchronous on that stream, never allocate, never synchronise.
+ *
+ * Two API levels:
+ *  - v1: the reference's exact symbol names and signatures (void return).
+ *    Errors print "Failed: ..." and exit(EXIT_FAILURE), the reference's
+ *    CUDACHECK convention (bagua-core-internal/cpp/include/bagua_utils.h:5).
+ *  - v2: `bagua_*` entry points returning a bagua_status_t, dtype-generic,
+ *    plus the bf16 and 1-bit sign+scale extensions and fused kernels.
+ *    v1 functions are thin wrappers over v2.
+ */
+#ifndef BAGUA_KERNELS_H
+#define BAGUA_KERNELS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* bagua_stream_t; /* hipStream_t */
+typedef uint16_t bagua_half_t; /* IEEE binary16 bits (reference `half`) */
+typedef uint16_t bagua_bf16_t; /* bfloat16 bits (extension) */
+
+/* dtype codes: reference BaguaTensorDtype F32/F16 (datatypes/mod.rs:40-47) + BF16 */
+enum { BAGUA_DTYPE_F32 = 0, BAGUA_DTYPE_F16 = 1, BAGUA_DTYPE_BF16 = 2 };
+
+typedef enum {
+    BAGUA_OK = 0,
+    BAGUA_ERR_INVALID_ARG = 1,  /* sizes / chunking / target out of range */
+    BAGUA_ERR_WORKSPACE = 2,    /* temp buffer too small */
+    BAGUA_ERR_HIP = 3,          /* kernel launch failed (see bagua_last_hip_error) */
+    BAGUA_ERR_UNSUPPORTED = 4   /* dtype not supported by this entry point */
+} bagua_status_t;
+
+const char* bagua_status_string(int status);
+int bagua_last_hip_error(void);
+
+/* ======================================================================== */
+/* v2 — MinMax-UInt8 codec (format: datatypes/mod.rs:669-704, K:455-500)     */
+/* ======================================================================== */
+/* Compressed bytes S = align32(chunk_size*num_chunks) + align32(2*sizeof T)*num_chunks
+ * (replaces MinMaxUInt8CompressionParameters::get_compressed_buffer_size, datatypes/mod.rs:669). */
+size_t bagua_minmax_u8_compressed_bytes(int dtype, int chunk_size, int num_chunks);
+/* Workspace for bagua_minmax_u8_compress (replaces the cub temp-size query, K:268-310). */
+size_t bagua_minmax_u8_workspace_bytes(int chunk_size, int num_chunks);
+/* compress_{f32,f16}_to_uint8_host (K:661-676): per-chunk min/max header + uint8 payload.
+ * target_chunk = -1 compresses all chunks, otherwise only chunk `target_chunk`. */
+int bagua_minmax_u8_compress(int dtype, const void* input, int input_num_element, int chunk_size,
+                             int num_chunks, uint8_t* output, size_t output_bytes, void* workspace,
+                             size_t workspace_bytes, int target_chunk, bagua_stream_t stream);
+/* The two passes of bagua_minmax_u8_compress launched separately (stage 1:
+ * per-workgroup min/max partials into `workspace`; stage 2: fold partials,
+ * header, quantise).  Same arguments in both calls; used for per-kernel
+ * timing and for overlapping the passes with other work. */
+int bagua_minmax_u8_compress_stage(int stage, int dtype, const void* input, int input_num_element,
+                                   int chunk_size, int num_chunks, uint8_t* output, size_t output_bytes,
+                                   void* workspace, size_t workspace_bytes, int target_chunk,
+                                   bagua_stream_t stream);
+/* decompress_uint8_to_{f32,f16}_host (K:667-681) */
+int bagua_minmax_u8_decompress(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                               int num_chunks, void* output, bagua_stream_t stream);
+
+/* ======================================================================== */
+/* v2 — 1-bit sign + scale codec (extension; format in DESIGN.md §4)         */
+/* ======================================================================== */
+size_t bagua_onebit_compressed_bytes(int chunk_size, int num_chunks);
+size_t bagua_onebit_workspace_bytes(int chunk_size, int num_chunks);
+int bagua_onebit_compress(int dtype, const void* input, int input_num_element, int chunk_size,
+                          int num_chunks, uint8_t* output, size_t output_bytes, void* workspace,
+                          size_t workspace_bytes, int target_chunk, bagua_stream_t stream);
+int bagua_onebit_decompress(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                            int num_chunks, void* output, bagua_stream_t stream);
+
+/* ======================================================================== */
+/* v2 — chunk reduction and elementwise ops                                  */
+/* ======================================================================== */
+/* reduce_{mean,sum}_{f32,f16}_inplace_host (K:646-660): chunk target_chunk =
+ * sum (or mean) of the num_chunks chunks, in the reference's summation order. */
+int bagua_reduce_chunks(int dtype, void* input, int chunk_size, int num_chunks, int target_chunk,
+                        int average, bagua_stream_t stream);
+/* Fused dequantise(num_chunks MinMax-UInt8 segments) + reduce into `output`
+ * (chunk_size elements), bit-identical to decompress + reduce_{mean,sum}. */
+int bagua_minmax_u8_decompress_reduce(int dtype, const uint8_t* input, size_t input_bytes,
+                                      int chunk_size, int num_chunks, void* output, int average,
+                                      bagua_stream_t stream);
+
+/* Middle step of the compressed centralized all-reduce
+ * (centralized_low_precision_synchronous.rs:40-60: decompress_from ->
+ * reduce_{mean,sum}_inplace(target) -> compress(target)) as two kernels:
+ * dequantise the num_chunks received segments of `input` and reduce them into
+ * chunk `target_chunk` of `tensor` (num_chunks*chunk_size elements), then
+ * requantise that chunk into segment `target_chunk` of `output` (a
+ * num_chunks-segment MinMax-UInt8 buffer of output_bytes).  Bit-identical to
+ * the unfused sequence.  Returns BAGUA_ERR_UNSUPPORTED when the shape has no
+ * vector path (num_chunks > 16 or misaligned); callers then run the unfused ops. */
+int bagua_minmax_u8_reduce_requantize(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                                      int num_chunks, void* tensor, int average, uint8_t* output,
+                                      size_t output_bytes, int target_chunk, void* workspace,
+                                      size_t workspace_bytes, bagua_stream_t stream);
+
+/* K:196-266 elementwise kernels, dtype-generic (f32, f16, bf16) */
+int bagua_add_inplace(int dtype, void* x, const void* y, int n, bagua_stream_t stream);
+int bagua_addmul_inplace(int dtype, void* x, const void* y, int n, float factor, bagua_stream_t stream);
+int bagua_substract_inplace(int dtype, void* x, const void* y, int n, bagua_stream_t stream);
+int bagua_average_inplace(int dtype, void* x, const void* y, int n, bagua_stream_t stream);
+int bagua_divide_inplace(int dtype, void* x, float d, int n, bagua_stream_t stream);
+
+/* ======================================================================== */
+/* v1 — the reference's extern "C" surface (K:573-691), same names/ABI       */
+/* ======================================================================== */
+void divide_inplace_f32_host(float* x, float D_, int N, bagua_stream_t stream);
+void divide_inplace_f16_host(bagua_half_t* x, float D_, int N, bagua_stream_t stream);
+void add_inplace_f32_host(float* x, float* y, int N, bagua_stream_t stream);
+void add_inplace_f16_host(bagua_half_t* x, bagua_half_t* y, int N, bagua_stream_t stream);
+void addmul_inplace_f32_host(float* x, float* y, int N, const float factor, bagua_stream_t stream);
+void addmul_inplace_f16_host(bagua_half_t* x, bagua_half_t* y, int N, const float factor,
+                             bagua_stream_t stream);
+void substract_inplace_f32_host(float* x, float* y, int N, bagua_stream_t stream);
+void substract_inplace_f16_host(bagua_half_t* x, bagua_half_t* y, int N, bagua_stream_t stream);
+void average_inplace_f32_host(float* x, float* y, int N, bagua_stream_t stream);
+void average_inplace_f16_host(bagua_half_t* x, bagua_half_t* y, int N, bagua_stream_t stream);
+void async_model_average_host(float* tensor, const float* reduced_tensor_copy,
+                              const float* tensor_copy, const float nranks, const int N,
+                              bagua_stream_t stream);
+void reduce_mean_f32_inplace_host(float* input, int chunk_size, int num_chunks, int target_chunk,
+                                  bagua_stream_t stream);
+void reduce_mean_f16_inplace_host(bagua_half_t* input, int chunk_size, int num_chunks,
+                                  int target_chunk, bagua_stream_t stream);
+void reduce_sum_f32_inplace_host(float* input, int chunk_size, int num_chunks, int target_chunk,
+                                 bagua_stream_t stream);
+void reduce_sum_f16_inplace_host(bagua_half_t* input, int chunk_size, int num_chunks,
+                                 int target_chunk, bagua_stream_t stream);
+void compress_f32_to_uint8_host(float* input, int input_num_element, int chunk_size,
+                                int num_chunks, uint8_t* output, size_t output_size,
+                                void* dev_buffer, size_t dev_size, int target_chunk,
+                                bagua_stream_t stream);
+void decompress_uint8_to_f32_host(uint8_t* input, size_t input_size, int chunk_size,
+                                  int num_chunks, float* output, bagua_stream_t stream);
+void compress_f16_to_uint8_host(bagua_half_t* input, int input_num_element, int chunk_size,
+                                int num_chunks, uint8_t* output, size_t output_size,
+                                void* dev_buffer, size_t dev_size, int target_chunk,
+                                bagua_stream_t stream);
+void decompress_uint8_to_f16_host(uint8_t* input, size_t input_size, int chunk_size,
+                                  int num_chunks, bagua_half_t* output, bagua_stream_t stream);
+size_t array_min_max_size_f32_host(float* input, int input_num_element, float* output,
+                                   bagua_stream_t stream);
+size_t array_min_max_size_f16_host(bagua_half_t* input, int input_num_element,
+                                   bagua_half_t* output, bagua_stream_t stream);
+
+/* v1-style extensions (same conventions as the v1 block) */
+void compress_bf16_to_uint8_host(bagua_bf16_t* input, int input_num_element, int chunk_size,
+                                 int num_chunks, uint8_t* output, size_t output_size,
+                                 void* dev_buffer, size_t dev_size, int target_chunk,
+                                 bagua_stream_t stream);
+void decompress_uint8_to_bf16_host(uint8_t* input, size_t input_size, int chunk_size,
+                                   int num_chunks, bagua_bf16_t* output, bagua_stream_t stream);
+size_t array_min_max_size_bf16_host(bagua_bf16_t* input, int input_num_element,
+                                    bagua_bf16_t* output, bagua_stream_t stream);
+void reduce_mean_bf16_inplace_host(bagua_bf16_t* input, int chunk_size, int num_chunks,
+                                   int target_chunk, bagua_stream_t stream);
+void reduce_sum_bf16_inplace_host(bagua_bf16_t* input, int chunk_size, int num_chunks,
+                                  int target_chunk, bagua_stream_t stream);
+void add_inplace_bf16_host(bagua_bf16_t* x, bagua_bf16_t* y, int N, bagua_stream_t stream);
+void addmul_inplace_bf16_host(bagua_bf16_t* x, bagua_bf16_t* y, int N, const float factor,
+                              bagua_stream_t stream);
+void compress_f32_to_onebit_host(float* input, int input_num_element, int chunk_size,
+                                 int num_chunks, uint8_t* output, size_t output_size,
+                                 void* dev_buffer, size_t dev_size, int target_chunk,
+                                 bagua_stream_t stream);
+void decompress_onebit_to_f32_host(uint8_t* input, size_t input_size, int chunk_size,
+                                   int num_chunks, float* output, bagua_stream_t stream);
+void compress_bf16_to_onebit_host(bagua_bf16_t* input, int input_num_element, int chunk_size,
+                                  int num_chunks, uint8_t* output, size_t output_size,
+                                  void* dev_buffer, size_t dev_size, int target_chunk,
+                                  bagua_stream_t stream);
+void decompress_onebit_to_bf16_host(uint8_t* input, size_t input_size, int chunk_size,
+                                    int num_chunks, bagua_bf16_t* output, bagua_stream_t stream);
+size_t onebit_temp_size_host(int chunk_size, int num_chunks);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BAGUA_KERNELS_H */
