@@ -26,6 +26,14 @@
 namespace bagua {
 
 constexpr int kVecPerBlockTile = kBlock * kSubtiles;  // 1024 x 16-B vectors = 16 KiB in flight per block
+// Launch shapes picked on MI355X with tools/stream_probe.hip:
+// the read-only min/max pass wants 8 vectors in flight per lane on 4 blocks
+// per CU; quantise 4 per lane on 8 blocks per CU; dequantise 4 per lane on
+// 16 blocks per CU (grid-strided).
+constexpr int kPartialsSub = 8;
+constexpr int kPartialsBlocks = 1024;
+constexpr int kQuantBlocks = 2048;
+constexpr int kDequantBlocks = 4096;
 
 __device__ __forceinline__ int64_t chunk_valid(int64_t in_num_elem, int64_t cs, int c) {
     // K:538-545: remaining elements, clamped to [0, chunk_size]
@@ -36,8 +44,8 @@ __device__ __forceinline__ int64_t chunk_valid(int64_t in_num_elem, int64_t cs, 
 template <typename T>
 __device__ __forceinline__ void fold(float f, uint32_t& lo, uint32_t& hi) {
     const int32_t k = f2key(f);
-    lo = min(lo, (uint32_t)(k - kKeyNegInf));
-    hi = min(hi, (uint32_t)(kKeyPosInf - k));
+    lo = min(lo, min_space_key(k));
+    hi = min(hi, max_space_key(k));
 }
 
 // ------------------------------------------------------------------------
@@ -53,33 +61,41 @@ __global__ __launch_bounds__(kBlock) void minmax_partials_kernel(
     const int64_t n = chunk_valid(in_num_elem, cs, c);
     const S* src = in + (int64_t)c * cs;
 
-    int64_t j0 = (int64_t)(((16u - ((uintptr_t)src & 15u)) & 15u) / sizeof(S));
+    // body starts on a 128-B line (head elements go to the scalar path)
+    int64_t j0 = (int64_t)(((128u - ((uintptr_t)src & 127u)) & 127u) / sizeof(S));
+    if (((uintptr_t)src % sizeof(S)) != 0) j0 = n;  // misaligned element pointer: all scalar
     if (j0 > n) j0 = n;
     const int64_t nvec = (n - j0) / N;
     const uint4* __restrict__ vsrc = reinterpret_cast<const uint4*>(src + j0);
 
     uint32_t lo = min_space(T::init_max());
     uint32_t hi = max_space(-T::init_max());
-    const int64_t stride = (int64_t)gridDim.x * kVecPerBlockTile;
-    for (int64_t base = (int64_t)blockIdx.x * kVecPerBlockTile; base < nvec; base += stride) {
-        uint4 r[kSubtiles];
-        bool ok[kSubtiles];
+    constexpr int SUB = kPartialsSub;
+    const int64_t stride = (int64_t)gridDim.x * kBlock * SUB;
+    for (int64_t base = (int64_t)blockIdx.x * kBlock * SUB; base < nvec; base += stride) {
+        if (base + kBlock * SUB <= nvec) {  // full tile: SUB loads in flight per lane
+            uint4 r[SUB];
 #pragma unroll
-        for (int k = 0; k < kSubtiles; ++k) {
-            const int64_t v = base + k * kBlock + threadIdx.x;
-            ok[k] = v < nvec;
-            if (ok[k]) r[k] = vsrc[v];  // default policy: pass 2 re-reads these lines
+            for (int k = 0; k < SUB; ++k) r[k] = vsrc[base + k * kBlock + threadIdx.x];  // default policy
+#pragma unroll
+            for (int k = 0; k < SUB; ++k) {
+                float f[N];
+                unpack16<T>(r[k], f);
+#pragma unroll
+                for (int i = 0; i < N; ++i) fold<T>(f[i], lo, hi);
+            }
+            continue;
         }
-#pragma unroll
-        for (int k = 0; k < kSubtiles; ++k) {
-            if (!ok[k]) continue;
+        for (int k = 0; k < SUB; ++k) {
+            const int64_t v = base + k * kBlock + threadIdx.x;
+            if (v >= nvec) continue;
             float f[N];
-            unpack16<T>(r[k], f);
+            unpack16<T>(vsrc[v], f);
 #pragma unroll
             for (int i = 0; i < N; ++i) fold<T>(f[i], lo, hi);
         }
     }
-    if (blockIdx.x == 0) {  // unaligned head and ragged tail (< 2N elements)
+    if (blockIdx.x == 0) {  // head before the first line and the ragged tail, scalar
         for (int64_t j = threadIdx.x; j < j0; j += kBlock) fold<T>(T::to_f(src[j]), lo, hi);
         for (int64_t j = j0 + nvec * N + threadIdx.x; j < n; j += kBlock) fold<T>(T::to_f(src[j]), lo, hi);
     }
@@ -162,22 +178,31 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
     const uint4* __restrict__ vsrc = reinterpret_cast<const uint4*>(src + j0);
     uint8_t* vdst = payload + j0;
     const int64_t ntiles = (nvec + kVecPerBlockTile - 1) / kVecPerBlockTile;
+    const bool all_valid = (n == cs);  // elements past in_num_elem quantise to 0
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int64_t base = (kReverse ? (ntiles - 1 - t) : t) * kVecPerBlockTile;
-        uint4 r[kSubtiles];
-        bool ok[kSubtiles];
+        if (all_valid && base + kVecPerBlockTile <= nvec) {
+            // full tile: all loads issued before any is consumed
+            uint4 r[kSubtiles];
 #pragma unroll
-        for (int k = 0; k < kSubtiles; ++k) {
-            const int64_t v = base + k * kBlock + threadIdx.x;
-            ok[k] = v < nvec;
-            if (ok[k]) r[k] = nt_load16(&vsrc[v]);
+            for (int k = 0; k < kSubtiles; ++k) r[k] = nt_load16(&vsrc[base + k * kBlock + threadIdx.x]);
+#pragma unroll
+            for (int k = 0; k < kSubtiles; ++k) {
+                const int64_t v = base + k * kBlock + threadIdx.x;
+                float f[N];
+                unpack16<T>(r[k], f);
+                uint32_t b[N];
+#pragma unroll
+                for (int i = 0; i < N; ++i) b[i] = quant(f[i], q);
+                store_bytes<T>(vdst + v * N, b);
+            }
+            continue;
         }
-#pragma unroll
-        for (int k = 0; k < kSubtiles; ++k) {
-            if (!ok[k]) continue;
+        for (int k = 0; k < kSubtiles; ++k) {  // ragged last tile / partially valid chunk
             const int64_t v = base + k * kBlock + threadIdx.x;
+            if (v >= nvec) continue;
             float f[N];
-            unpack16<T>(r[k], f);
+            unpack16<T>(nt_load16(&vsrc[v]), f);
             uint32_t b[N];
             const int64_t jv = j0 + v * N;
 #pragma unroll
@@ -219,22 +244,33 @@ __global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
     uint4* __restrict__ vdst = reinterpret_cast<uint4*>(dst + j0);
     const uint8_t* vsrc = payload + j0;
     const int64_t stride = (int64_t)gridDim.x * kVecPerBlockTile;
+    using W = typename Vec<T>::out_bytes;  // the N payload bytes of one vector
     for (int64_t base = (int64_t)blockIdx.x * kVecPerBlockTile; base < nvec; base += stride) {
-        uint32_t b[kSubtiles][N];
-        bool ok[kSubtiles];
+        if (base + kVecPerBlockTile <= nvec) {
+            // full tile: raw loads first (no unpacking inside the load block, or
+            // each load gets its own vmcnt(0) wait), then dequantise and store
+            W raw[kSubtiles];
 #pragma unroll
-        for (int k = 0; k < kSubtiles; ++k) {
-            const int64_t v = base + k * kBlock + threadIdx.x;
-            ok[k] = v < nvec;
-            if (ok[k]) load_bytes<T>(vsrc + v * N, b[k]);
+            for (int k = 0; k < kSubtiles; ++k) raw[k] = load_word<T>(vsrc + (base + k * kBlock + threadIdx.x) * N);
+#pragma unroll
+            for (int k = 0; k < kSubtiles; ++k) {
+                uint32_t b[N];
+                split_bytes<T>(raw[k], b);
+                float f[N];
+#pragma unroll
+                for (int i = 0; i < N; ++i) f[i] = dequant(b[i], q);
+                nt_store16(pack16<T>(f), &vdst[base + k * kBlock + threadIdx.x]);
+            }
+            continue;
         }
-#pragma unroll
         for (int k = 0; k < kSubtiles; ++k) {
-            if (!ok[k]) continue;
             const int64_t v = base + k * kBlock + threadIdx.x;
+            if (v >= nvec) continue;
+            uint32_t b[N];
+            split_bytes<T>(load_word<T>(vsrc + v * N), b);
             float f[N];
 #pragma unroll
-            for (int i = 0; i < N; ++i) f[i] = dequant(b[k][i], q);
+            for (int i = 0; i < N; ++i) f[i] = dequant(b[i], q);
             nt_store16(pack16<T>(f), &vdst[v]);
         }
     }
@@ -248,10 +284,13 @@ __global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
 // ------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------
-static int blocks_for(int64_t elems, int per_vec, int nact) {
+// workgroups per chunk: one per tile of (kBlock * sub) vectors, capped so the
+// whole launch has about `target` workgroups (the rest grid-strides)
+static int blocks_for(int64_t elems, int per_vec, int nact, int sub = kSubtiles, int target = kQuantBlocks) {
     const int64_t nvec = elems / per_vec + 1;
-    int64_t tiles = (nvec + kVecPerBlockTile - 1) / kVecPerBlockTile;
-    const int64_t per_chunk = (kTargetBlocks + nact - 1) / nact;
+    const int64_t tile = (int64_t)kBlock * sub;
+    int64_t tiles = (nvec + tile - 1) / tile;
+    const int64_t per_chunk = (target + nact - 1) / nact;
     if (tiles > per_chunk) tiles = per_chunk;
     return (int)(tiles < 1 ? 1 : tiles);
 }
@@ -268,7 +307,7 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
     const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);  // K:537
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     const int nact = target < 0 ? p : 1;
-    int nblk = blocks_for(cs, Vec<T>::N, nact);
+    int nblk = blocks_for(cs, Vec<T>::N, nact, kPartialsSub, kPartialsBlocks);
     const int64_t cap = ws ? (int64_t)(ws_bytes / sizeof(uint2)) / nact : 0;
     if (cap < 1) return BAGUA_ERR_WORKSPACE;
     if (nblk > cap) nblk = (int)cap;
@@ -316,7 +355,8 @@ static int decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p, vo
     if (p <= 0 || p > 65535 || cs < 0 || !in || !out) return BAGUA_ERR_INVALID_ARG;
     const int64_t chunk_offset = (int64_t)(in_bytes / (size_t)p);  // K:566
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
-    hipLaunchKernelGGL(minmax_dequantize_kernel<T>, dim3(blocks_for(cs, Vec<T>::N, p), p), dim3(kBlock), 0,
+    hipLaunchKernelGGL(minmax_dequantize_kernel<T>,
+                       dim3(blocks_for(cs, Vec<T>::N, p, kSubtiles, kDequantBlocks), p), dim3(kBlock), 0,
                        s, in, chunk_offset, (int64_t)cs, static_cast<S*>(out));
     return check_launch();
 }

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
                 if (c >= p) break;
                 const QParams q = qp[c];
 #pragma unroll
-                for (int i = 0; i < N; ++i) s[i][y] = s[i][y] + dequant(b[y][i], q);
+                for (int i = 0; i < N; ++i) s[i][y] = s[i][y] + as_stored<T>(dequant(b[y][i], q));
             }
         }
         float o[N];
@@ -192,8 +192,8 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
             for (int i = 0; i < N; ++i) {
                 const int32_t k = f2key(st[i]);
                 if (st[i] == st[i]) {
-                    lo = min(lo, (uint32_t)(k - kKeyNegInf));
-                    hi = min(hi, (uint32_t)(kKeyPosInf - k));
+                    lo = min(lo, min_space_key(k));
+                    hi = min(hi, max_space_key(k));
                 }
             }
         }
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
         for (int y = 0; y < BY; ++y) s[y] = 0.0f;
         for (int c = 0; c < p; ++c) {
             const int y = c % BY;
-            s[y] = s[y] + dequant(in[(int64_t)c * chunk_offset + 32 + j], qp[c]);
+            s[y] = s[y] + as_stored<T>(dequant(in[(int64_t)c * chunk_offset + 32 + j], qp[c]));
         }
         tree_finish<BY>(s);
         const S o = T::from_f(AVG ? s[0] / pf : s[0]);
@@ -214,8 +214,8 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
             const float st = T::to_f(o);
             if (st == st) {
                 const int32_t k = f2key(st);
-                lo = min(lo, (uint32_t)(k - kKeyNegInf));
-                hi = min(hi, (uint32_t)(kKeyPosInf - k));
+                lo = min(lo, min_space_key(k));
+                hi = min(hi, max_space_key(k));
             }
         }
     }

@@ -1,0 +1,75 @@
+"""Worker of tests/test_distributed_sim.py: one rank of the compressed comm
+ops over torch.distributed (gloo, CPU), computing with the C oracle.
+
+This is the multi-rank rehearsal of the RCCL path: the same op order as
+bagua-core_amd/csrc/runtime/comm_ops.cpp (compress -> out-of-place alltoall
+-> dequantise+reduce -> requantise own chunk -> in-place allgather ->
+decompress; ring send/recv for the decentralized op), with real collectives
+moving the real compressed bytes between processes.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from oracle import oracle_c as C
+
+
+def centralized_rank(rank: int, world: int, port: int, inputs_path: str, out_dir: str, dtype: int) -> None:
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        with np.load(inputs_path, allow_pickle=False) as z:
+            t = z[f"x{rank}"].copy()
+        p = world
+        send = C.compress_minmax_u8(t, dtype, p, -1)
+        S = send.size
+        assert S % p == 0
+        recv = torch.empty(S, dtype=torch.uint8)
+        dist.all_to_all_single(recv, torch.from_numpy(send))
+        C.decompress_minmax_u8(recv.numpy(), p, t, dtype)
+        C.reduce_chunks(t, dtype, p, rank, True)
+        C.compress_minmax_u8(t, dtype, p, rank, out=send)
+        cnt = S // p
+        gathered = torch.empty(S, dtype=torch.uint8)
+        dist.all_gather_into_tensor(gathered, torch.from_numpy(send[rank * cnt:(rank + 1) * cnt].copy()))
+        C.decompress_minmax_u8(gathered.numpy(), p, t, dtype)
+        np.save(os.path.join(out_dir, f"out{rank}.npy"), t.view(np.uint8))
+    finally:
+        dist.destroy_process_group()
+
+
+def decentralized_rank(rank: int, world: int, port: int, inputs_path: str, out_dir: str, dtype: int) -> None:
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        with np.load(inputs_path, allow_pickle=False) as z:
+            t, w, l, r = (z[f"{k}{rank}"].copy() for k in "twlr")
+        f13, f53 = float(np.float32(1.0 / 3.0)), float(np.float32(-5.0 / 3.0))
+        C.addmul_inplace(t, l, dtype, f13)
+        C.addmul_inplace(t, r, dtype, f13)
+        C.addmul_inplace(t, w, dtype, f53)
+        mine = C.compress_minmax_u8(t, dtype, 1, -1)
+        lpeer, rpeer = (rank + world - 1) % world, (rank + 1) % world
+        lbuf, rbuf = torch.empty(mine.size, dtype=torch.uint8), torch.empty(mine.size, dtype=torch.uint8)
+        m = torch.from_numpy(mine)
+        reqs = [dist.isend(m, lpeer, tag=1), dist.isend(m, rpeer, tag=2),
+                dist.irecv(lbuf, lpeer, tag=2), dist.irecv(rbuf, rpeer, tag=1)]
+        for q in reqs:
+            q.wait()
+        C.decompress_minmax_u8(lbuf.numpy(), 1, t, dtype)
+        C.add_inplace(l, t, dtype)
+        C.decompress_minmax_u8(rbuf.numpy(), 1, t, dtype)
+        C.add_inplace(r, t, dtype)
+        C.decompress_minmax_u8(mine, 1, t, dtype)
+        C.add_inplace(t, w, dtype)
+        w[...] = t
+        np.savez(os.path.join(out_dir, f"dec{rank}.npz"), t=t.view(np.uint8), w=w.view(np.uint8),
+                 l=l.view(np.uint8), r=r.view(np.uint8))
+    finally:
+        dist.destroy_process_group()

@@ -140,7 +140,9 @@ def test_invalid_arguments_are_reported(bc):
         t.compress("TopK", 1, -1)
     K = bc._native.K
     assert K.bagua_minmax_u8_compress(F32, None, 0, 0, 0, None, 0, None, 0, -1, None) == 1
-    assert K.bagua_minmax_u8_compress(F32, t.data_ptr(), 10, 10, 1, t.data_ptr(), 64, None, 0, -1, None) == 1
+    assert K.bagua_minmax_u8_compress(F32, t.data_ptr(), 10, 10, 1, t.data_ptr(), 64, None, 0, -1, None) == 2
+    assert K.bagua_minmax_u8_compress(F32, t.data_ptr(), 10, 10, 1, t.data_ptr(), 41, t.data_ptr(), 64, -1,
+                                      None) == 1  # output smaller than chunk_size + 32
 
 
 # ---------------------------------------------------------------- reduce ----

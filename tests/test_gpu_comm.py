@@ -1,0 +1,139 @@
+"""GPU tests of the comm ops through RCCL on a single-rank communicator
+(the GPU box has one MI355X; multi-rank semantics are covered on CPU with
+gloo in tests/test_distributed_sim.py and by construction), and of the
+bucket / scheduler surface.  Results are compared bit-exact with the oracle
+simulation of the reference op sequence (oracle/simulate.py)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle_np as NP
+from oracle import simulate
+
+pytestmark = pytest.mark.gpu
+
+F32, F16, BF16 = 0, 1, 2
+TORCH = {F32: torch.float32, F16: torch.float16, BF16: torch.bfloat16}
+STORAGE = {F32: np.float32, F16: np.float16, BF16: np.uint16}
+
+
+@pytest.fixture(scope="module")
+def bc():
+    import bagua_core
+    return bagua_core
+
+
+@pytest.fixture(scope="module")
+def comm(bc):
+    stream = torch.cuda.Stream()
+    uid = bc.BaguaSingleCommunicatorPy.generate_nccl_unique_id_str()
+    c = bc.BaguaSingleCommunicatorPy(0, 1, 0, stream.cuda_stream, uid)
+    c._keep_stream = stream
+    return c
+
+
+def dev(x, dtype):
+    if dtype == BF16:
+        return torch.from_numpy(x.view(np.int16).copy()).view(torch.bfloat16).cuda()
+    return torch.from_numpy(x.copy()).cuda()
+
+
+def host(t, dtype):
+    torch.cuda.synchronize()
+    if dtype == BF16:
+        return t.view(torch.int16).cpu().numpy().view(np.uint16)
+    return t.cpu().numpy()
+
+
+def test_communicator_basics(bc, comm):
+    assert comm.nranks() == 1 and comm.rank() == 0
+    assert not comm.check_abort()
+    uid = bc.BaguaSingleCommunicatorPy.generate_nccl_unique_id_str()
+    import base64
+    assert len(base64.b64decode(uid)) == 128  # communicators/mod.rs:226-240
+    t = torch.arange(16, dtype=torch.float32, device="cuda")
+    bt = bc.BaguaTensorPy(t, "t")
+    comm.allreduce_inplace(bt, 0)
+    comm.allgather_inplace(bt)
+    comm.alltoall_inplace(bt)
+    comm.barrier()
+    assert torch.equal(t.cpu(), torch.arange(16, dtype=torch.float32))
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16, F16])
+@pytest.mark.parametrize("fused", [True, False])
+def test_centralized_low_precision_p1(bc, comm, oracle_c, dtype, fused):
+    """Config 1 (loopback, p = 1) on the GPU through RCCL: bit-exact with the reference sequence."""
+    rng = np.random.default_rng(21 + dtype)
+    x = NP.from_f32((rng.standard_normal(1 << 18) * 1e-3).astype(np.float32), dtype)
+    want = simulate.centralized_low_precision(oracle_c, [x], dtype, True)[0]
+    t = dev(x, dtype)
+    b = bc.BaguaBucketPy("b", [bc.BaguaTensorPy(t, "t")])
+    b.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+    b._ops[0].fused = fused
+    b.execute_ops()
+    assert np.array_equal(host(t, dtype).view(np.uint8), want.view(np.uint8))
+
+
+def test_full_precision_p1(bc, comm):
+    t = torch.randn(4096, device="cuda")
+    ref = t.clone()
+    b = bc.BaguaBucketPy("b", [bc.BaguaTensorPy(t, "t")])
+    b.append_centralized_synchronous_op(comm, None, False, True, False, None)
+    b.execute_ops()
+    assert torch.equal(t, ref)
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+def test_decentralized_low_precision_p1(bc, comm, oracle_c, dtype):
+    rng = np.random.default_rng(31 + dtype)
+    n = 100003
+    arrs = [NP.from_f32((rng.standard_normal(n) * 1e-3).astype(np.float32), dtype) for _ in range(4)]
+    want = simulate.decentralized_low_precision(oracle_c, [arrs[0]], [arrs[1]], [arrs[2]], [arrs[3]], dtype)
+    ts = [dev(a, dtype) for a in arrs]
+    bt = [bc.BaguaTensorPy(x, nm) for x, nm in zip(ts, ["t", "w", "l", "r"])]
+    b = bc.BaguaBucketPy("b", [bt[0]])
+    b.append_low_precision_decentralized_synchronous_op(comm, None, False, "ring", "MinMaxUInt8", bt[1], bt[2], bt[3])
+    b.execute_ops()
+    for got, w in zip(ts, want):
+        assert np.array_equal(host(got, dtype).view(np.uint8), w[0].view(np.uint8))
+
+
+def test_backend_schedules_noncontiguous_bucket(bc, comm, oracle_c):
+    """Two non-adjacent tensors in one bucket: flattened, reduced, copied back
+    (datatypes/mod.rs:963-1070), driven by BaguaCommBackendPy readiness."""
+    rng = np.random.default_rng(41)
+    a = (rng.standard_normal(3000) * 1e-3).astype(np.float32)
+    c = (rng.standard_normal(5000) * 1e-3).astype(np.float32)
+    want = simulate.centralized_low_precision(oracle_c, [np.concatenate([a, c])], F32, True)[0]
+    ta, tc = dev(a, F32), dev(c, F32)
+    _gap = torch.empty(1000, device="cuda")  # keep the two allocations apart
+    ba, bc_ = bc.BaguaTensorPy(ta, "a"), bc.BaguaTensorPy(tc, "c")
+    bucket = bc.BaguaBucketPy("bucket0", [ba, bc_])
+    bucket.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+    backend = bc.BaguaCommBackendPy(10, 0)
+    backend.register_ordered_buckets([bucket])
+    ev = torch.cuda.Event()
+    ev.record()
+    backend.mark_communication_ready(ba, ev.cuda_event)
+    assert backend.wait_pending_comm_ops() == 0  # not ready until every tensor is
+    backend.mark_communication_ready(bc_, 0)
+    assert backend.wait_pending_comm_ops() == 1
+    got = np.concatenate([host(ta, F32), host(tc, F32)])
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    with pytest.raises(RuntimeError):
+        backend.register_ordered_buckets([bucket, bc.BaguaBucketPy("dup", [ba])])
+    del _gap
+
+
+def test_pool_reuse(bc):
+    N = bc._native
+    import ctypes
+    p1 = ctypes.c_uint64()
+    assert N.C.bagua_pool_alloc(0, 1 << 20, ctypes.byref(p1)) == 0
+    assert N.C.bagua_pool_free(p1.value) == 0
+    p2 = ctypes.c_uint64()
+    assert N.C.bagua_pool_alloc(0, (1 << 20) - 100, ctypes.byref(p2)) == 0
+    assert p2.value == p1.value  # same size class -> block reused
+    assert N.C.bagua_pool_free(p2.value) == 0
+    assert N.C.bagua_pool_free(12345) != 0
