@@ -207,17 +207,20 @@ __device__ __forceinline__ void nt_store8(const uint2& v, void* p) {
     __builtin_nontemporal_store(w, reinterpret_cast<u32x2*>(p));
 }
 
-// N quantised bytes <-> one 4-B (f32) or 8-B (16-bit) non-temporal access
-// (measured: nt stores of the 4-B byte words are ~18 % faster than plain)
+// N quantised bytes -> one 4-B (f32) or 8-B (16-bit) access.  PLAIN stores on
+// purpose: the compressed payload (1/4 of the input) then stays in L2 / the
+// 256 MiB Infinity Cache for whoever reads it next (the decode, RCCL).  The
+// whole-step cache-policy sweep (tools/policy_probe.hip) put
+// this at 142 us vs 152 us with nt stores, although nt is faster in isolation.
 template <typename T>
 __device__ __forceinline__ void store_bytes(uint8_t* p, uint32_t (&b)[Vec<T>::N]) {
     if constexpr (Vec<T>::N == 4) {
-        __builtin_nontemporal_store(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24), reinterpret_cast<uint32_t*>(p));
+        *reinterpret_cast<uint32_t*>(p) = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
     } else {
         uint2 v;
         v.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
         v.y = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
-        nt_store8(v, p);
+        *reinterpret_cast<uint2*>(p) = v;
     }
 }
 

@@ -177,6 +177,47 @@ __global__ __launch_bounds__(256) void deq16_k(const u32x4* __restrict__ in, u32
     }
 }
 
+// q read from a device header per block (like the product), optionally forced uniform
+template <bool UNIFORM>
+__global__ __launch_bounds__(256) void deq4_hdr_k(const uint32_t* __restrict__ in, u32x4* __restrict__ out, int64_t nvec,
+                                                  const float* hdr) {
+    Q q{hdr[0], hdr[1], hdr[2]};
+    if constexpr (UNIFORM) {
+        q.scale = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, q.scale)));
+        q.lb = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, q.lb)));
+    }
+    for (int64_t base = (int64_t)blockIdx.x * 1024; base < nvec; base += (int64_t)gridDim.x * 1024) {
+        uint32_t b[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) b[k] = __builtin_nontemporal_load(in + base + k * 256 + threadIdx.x);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            u32x4 o = {__float_as_uint(dequant(b[k] & 0xff, q)), __float_as_uint(dequant((b[k] >> 8) & 0xff, q)),
+                       __float_as_uint(dequant((b[k] >> 16) & 0xff, q)), __float_as_uint(dequant(b[k] >> 24, q))};
+            __builtin_nontemporal_store(o, out + base + k * 256 + threadIdx.x);
+        }
+    }
+}
+
+// 256-entry table of the exactly-divided values in LDS: no division per element
+__global__ __launch_bounds__(256) void deq4_lut_k(const uint32_t* __restrict__ in, u32x4* __restrict__ out, int64_t nvec,
+                                                  Q q) {
+    __shared__ float lut[256];
+    lut[threadIdx.x] = dequant(threadIdx.x, q);
+    __syncthreads();
+    for (int64_t base = (int64_t)blockIdx.x * 1024; base < nvec; base += (int64_t)gridDim.x * 1024) {
+        uint32_t b[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) b[k] = __builtin_nontemporal_load(in + base + k * 256 + threadIdx.x);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            u32x4 o = {__float_as_uint(lut[b[k] & 0xff]), __float_as_uint(lut[(b[k] >> 8) & 0xff]),
+                       __float_as_uint(lut[(b[k] >> 16) & 0xff]), __float_as_uint(lut[b[k] >> 24])};
+            __builtin_nontemporal_store(o, out + base + k * 256 + threadIdx.x);
+        }
+    }
+}
+
 // ---- min/max read pass ---------------------------------------------------------
 __device__ __forceinline__ int32_t key(float f) { int32_t i = __float_as_int(f); return i ^ ((i >> 31) & 0x7fffffff); }
 template <int SUB, bool NTL>
@@ -299,6 +340,28 @@ int main(int argc, char** argv) {
     add("PRODUCT dequantize raw-launch g2048", B + W, [=](int) {
         hipLaunchKernelGGL(bagua::minmax_dequantize_kernel<bagua::F32>, dim3(2048, 1), dim3(256), 0, nullptr,
                            comp, (int64_t)S, (int64_t)n, (float*)y); });
+    float* hdr;
+    CK(hipMalloc(&hdr, 16));
+    {
+        float h[4] = {q.scale, q.lb, q.ub, 0};
+        CK(hipMemcpy(hdr, h, 16, hipMemcpyHostToDevice));
+    }
+    for (int g : {2048, 4096}) {
+        add("deq4 hdr(vgpr q)        g" + std::to_string(g), B + W, [=](int) { deq4_hdr_k<false><<<g, 256>>>((uint32_t*)bytes, y, nvec, hdr); });
+        add("deq4 hdr(readfirstlane) g" + std::to_string(g), B + W, [=](int) { deq4_hdr_k<true><<<g, 256>>>((uint32_t*)bytes, y, nvec, hdr); });
+        add("deq4 lut                g" + std::to_string(g), B + W, [=](int) { deq4_lut_k<<<g, 256>>>((uint32_t*)bytes, y, nvec, q); });
+    }
+    // order effects: what ran just before changes the cache state the next kernel sees
+    add("ORDER pre: write y", W, [=](int) { write_k<4, false><<<4096, 256>>>(y, nvec); });
+    add("ORDER deq4 nt/nt after write y", B + W, [=](int) { deq4_k<4, true, true><<<4096, 256>>>((uint32_t*)bytes, y, nvec, q); });
+    add("ORDER deq4 nt/nt again", B + W, [=](int) { deq4_k<4, true, true><<<4096, 256>>>((uint32_t*)bytes, y, nvec, q); });
+    add("ORDER deq4 lut after deq4", B + W, [=](int) { deq4_lut_k<<<4096, 256>>>((uint32_t*)bytes, y, nvec, q); });
+    add("ORDER pre: read x", R, [=](int) { read_k<4, false><<<4096, 256>>>(x, sink, nvec); });
+    add("ORDER deq4 lut after read x", B + W, [=](int) { deq4_lut_k<<<4096, 256>>>((uint32_t*)bytes, y, nvec, q); });
+    add("ORDER pre: quant4 (writes bytes)", R + B, [=](int) { quant4_k<4, true, true, true><<<2048, 256>>>(x, (uint32_t*)bytes, nvec, q); });
+    add("ORDER deq4 nt/nt after quant", B + W, [=](int) { deq4_k<4, true, true><<<4096, 256>>>((uint32_t*)bytes, y, nvec, q); });
+    add("ORDER pre: quant4 again", R + B, [=](int) { quant4_k<4, true, true, true><<<2048, 256>>>(x, (uint32_t*)bytes, nvec, q); });
+    add("ORDER PRODUCT dequantize after quant", B + W, [=](int) { bagua_minmax_u8_decompress(0, comp, S, (int)n, 1, y, nullptr); });
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));

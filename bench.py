@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--workload", choices=["auto", "codec", "allreduce", "onebit"], default="auto")
     ap.add_argument("--elements", type=int, default=0, help="override bucket elements")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=4.0, help="wall budget of the cpu_baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the cpu_baseline leg")
     return ap.parse_args()
 
 
@@ -173,7 +173,7 @@ def cpu_baseline(args, sample_elems: int = 1 << 24):
         oracle_c.decompress_minmax_u8(buf, 1, out, 0)
         reps += 1
         el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or reps >= 200:
+        if el >= args.cpu_seconds or reps >= 100000:
             break
     return {"value": round(4.0 * sample_elems * reps / el / GiB, 3), "unit": "GiB/s", "cores": lib_threads,
             "kind": "port",
