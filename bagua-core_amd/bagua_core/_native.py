@@ -137,6 +137,9 @@ CORE_SIGNATURES = {
     "bagua_comm_group_end": (_i32, []),
     "bagua_comm_barrier": (_i32, [_C]),
     "bagua_comm_synchronize": (_i32, [_C]),
+    "bagua_loopback_group_create": (_vp, [_i32, _i32]),
+    "bagua_loopback_group_destroy": (None, [_vp]),
+    "bagua_loopback_communicator_create": (_C, [_vp, _sz, _u64]),
     "bagua_centralized_low_precision_synchronous": (_i32, [_C, _T, _i32, _i32]),
     "bagua_centralized_low_precision_synchronous_unfused": (_i32, [_C, _T, _i32, _i32]),
     "bagua_centralized_full_precision_synchronous": (_i32, [_C, _T, _i32]),

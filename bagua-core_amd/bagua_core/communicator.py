@@ -30,6 +30,14 @@ class BaguaSingleCommunicatorPy:
         if h is not None and h.value:
             N.C.bagua_single_communicator_c_destroy(ctypes.byref(h))
 
+    @classmethod
+    def _from_handle(cls, handle: int, rank: int, nranks: int, device_id: int, stream_ptr: int, keep=()):
+        obj = cls.__new__(cls)
+        obj._rank, obj._nranks, obj._device_id, obj._stream_ptr = rank, nranks, device_id, stream_ptr
+        obj._handle = ctypes.c_void_p(handle)
+        obj._keep = keep
+        return obj
+
     @staticmethod
     def generate_nccl_unique_id_str() -> str:
         buf = ctypes.create_string_buffer(512)
@@ -97,3 +105,31 @@ class BaguaSingleCommunicatorPy:
 
     def synchronize(self) -> None:
         N.check(N.C.bagua_comm_synchronize(self._handle), "stream synchronize")
+
+
+class _LoopbackGroup:
+    def __init__(self, nranks: int, device_id: int):
+        self.handle = N.C.bagua_loopback_group_create(nranks, device_id)
+        if not self.handle:
+            raise RuntimeError("cannot create loopback group")
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            N.C.bagua_loopback_group_destroy(self.handle)
+            self.handle = None
+
+
+def loopback_communicators(nranks: int, device_id: int = 0) -> list:
+    """`nranks` communicators of an in-process loopback group on one device
+    (test harness: drive each from its own thread; see bagua_core.h)."""
+    import torch
+    group = _LoopbackGroup(nranks, device_id)
+    comms = []
+    for r in range(nranks):
+        stream = torch.cuda.Stream(device=device_id)
+        h = N.C.bagua_loopback_communicator_create(group.handle, r, stream.cuda_stream)
+        if not h:
+            raise RuntimeError("cannot create loopback communicator")
+        comms.append(BaguaSingleCommunicatorPy._from_handle(h, r, nranks, device_id, stream.cuda_stream,
+                                                            keep=(group, stream)))
+    return comms

@@ -1,21 +1,47 @@
-// comm_internal.hpp — communicator internals shared by communicator.cpp and comm_ops.cpp.
+// comm_internal.hpp — the transport behind a communicator.
+//
+// The comm ops (comm_ops.cpp) are written against this interface.  Product
+// communicators use RcclTransport (RCCL over xGMI).  LoopbackTransport runs p
+// virtual ranks as p host threads on ONE device, with collectives as
+// device-to-device copies: it executes the very same op code at p > 1 on a
+// one-GPU box, which is how the multi-rank path is parity-tested there.
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <cstddef>
+
+namespace bagua {
+
+struct Transport {
+    virtual ~Transport() = default;
+    // count is in elements of `dtype` (bagua dtype codes)
+    virtual int allreduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t s) = 0;
+    virtual int broadcast(void* buf, size_t count, int dtype, int root, hipStream_t s) = 0;
+    // block j of `send` (count elements at j*count) goes to rank j; block j of `recv` comes from rank j
+    virtual int alltoall(const void* send, void* recv, size_t count, int dtype, hipStream_t s) = 0;
+    // rank j's `count` elements land at recv + j*count (in place when send == recv + rank*count)
+    virtual int allgather(const void* send, void* recv, size_t count, int dtype, hipStream_t s) = 0;
+    virtual int send(const void* buf, size_t count, int dtype, int peer, hipStream_t s) = 0;
+    virtual int recv(void* buf, size_t count, int dtype, int peer, hipStream_t s) = 0;
+    virtual int group_start() = 0;
+    virtual int group_end() = 0;
+    virtual int abort() = 0;
+};
+
+Transport* make_rccl_transport(ncclComm_t comm);
+ncclDataType_t nccl_dtype(int d);
+int nccl_status(ncclResult_t r);
+
+}  // namespace bagua
 
 struct BaguaSingleCommunicatorC {
-    ncclComm_t comm = nullptr;
+    bagua::Transport* t = nullptr;
     size_t rank = 0;
     size_t nranks = 1;
     int device_id = 0;
     hipStream_t stream = nullptr;
     std::atomic<bool> aborted{false};
 };
-
-namespace bagua {
-ncclDataType_t nccl_dtype(int d);
-int nccl_status(ncclResult_t r);
-}  // namespace bagua

@@ -35,7 +35,7 @@ struct Chunking {
 };
 
 int plan(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int method, Chunking* k) {
-    if (!c || !c->comm || !t) return BAGUA_ERR_INVALID_ARG;
+    if (!c || !c->t || !t) return BAGUA_ERR_INVALID_ARG;
     if (c->aborted.load()) return BAGUA_ERR_ABORTED;
     k->p = (int)c->nranks;
     k->rank = (int)c->rank;
@@ -83,7 +83,7 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
     // 1. compress every chunk (target -1)
     TRY(bagua_tensor_compress_into(t, method, k.p, s, -1, &sv));
     // 2. alltoall: slot j of recv <- rank j's segment `rank`
-    TRY(nccl_status(ncclAllToAll(send.as<void>(), recv.as<void>(), k.S / k.p, ncclUint8, c->comm, c->stream)));
+    TRY(c->t->alltoall(send.as<void>(), recv.as<void>(), k.S / k.p, BAGUA_DTYPE_U8, c->stream));
     // 3. reduce the p received versions of the own chunk and requantise it into send[rank]
     bool done = false;
     if (fused && method == BAGUA_COMPRESSION_MINMAX_UINT8) {
@@ -131,7 +131,7 @@ int bagua_centralized_full_precision_synchronous(BaguaSingleCommunicatorC* c, co
 int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t,
                                                   const bagua_tensor_t* weight, const bagua_tensor_t* left,
                                                   const bagua_tensor_t* right, int method) {
-    if (!c || !c->comm || !t || !weight || !left || !right) return BAGUA_ERR_INVALID_ARG;
+    if (!c || !c->t || !t || !weight || !left || !right) return BAGUA_ERR_INVALID_ARG;
     if (c->aborted.load()) return BAGUA_ERR_ABORTED;
     DeviceGuard guard(c->device_id);
     const uint64_t s = (uint64_t)(uintptr_t)c->stream;
@@ -155,12 +155,12 @@ int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* c, c
     // :98-115 ring exchange inside one group
     const int p = (int)c->nranks, r = (int)c->rank;
     const int lpeer = (r + p - 1) % p, rpeer = (r + 1) % p;
-    TRY(bagua_comm_group_start());
+    TRY(c->t->group_start());
     rc = bagua_comm_send(c, &mv, lpeer);
     if (!rc) rc = bagua_comm_send(c, &mv, rpeer);
     if (!rc) rc = bagua_comm_recv(c, &lv, lpeer);
     if (!rc) rc = bagua_comm_recv(c, &rv, rpeer);
-    const int rc_end = bagua_comm_group_end();
+    const int rc_end = c->t->group_end();
     if (rc || rc_end) return finish(c, rc ? rc : rc_end);
     // :126-151
     TRY(bagua_tensor_decompress_from(t, method, 1, &lv, s));

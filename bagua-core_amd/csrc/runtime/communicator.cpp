@@ -3,13 +3,13 @@
 // bagua-core-c/src/lib.rs:9-69, whose symbols were Rust-mangled: exported
 // unmangled here).
 //
-// One communicator = one ncclComm_t + the stream every collective and codec
-// kernel of the comm ops is enqueued on (the reference binds an
-// Al::NCCLCommunicator to a stream the same way, communicators/mod.rs:44).
+// One communicator = one transport (an ncclComm_t for the product) + the
+// stream every collective and codec kernel of the comm ops is enqueued on
+// (the reference binds an Al::NCCLCommunicator to a stream the same way,
+// communicators/mod.rs:44).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
-#include <atomic>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -40,10 +40,9 @@ bool base64_decode(const char* s, std::vector<uint8_t>* out) {
     out->clear();
     uint32_t v = 0;
     int bits = 0;
-    for (; *s; ++s) {
-        if (*s == '=') break;
+    for (; *s && *s != '='; ++s) {
         const char* f = std::strchr(kB64, *s);
-        if (!f || !*s) return false;
+        if (!f) return false;
         v = (v << 6) | (uint32_t)(f - kB64);
         bits += 6;
         if (bits >= 8) {
@@ -82,14 +81,54 @@ int nccl_status(ncclResult_t r) {
     return BAGUA_ERR_COMM;
 }
 
+// ------------------------------------------------------------ RCCL transport --
+class RcclTransport final : public Transport {
+   public:
+    explicit RcclTransport(ncclComm_t c) : comm_(c) {}
+    ~RcclTransport() override {
+        if (comm_) (void)ncclCommDestroy(comm_);
+    }
+    int allreduce(const void* s, void* r, size_t n, int d, int op, hipStream_t st) override {
+        return nccl_status(ncclAllReduce(s, r, n, nccl_dtype(d), nccl_op(op), comm_, st));
+    }
+    int broadcast(void* b, size_t n, int d, int root, hipStream_t st) override {
+        return nccl_status(ncclBroadcast(b, b, n, nccl_dtype(d), root, comm_, st));
+    }
+    int alltoall(const void* s, void* r, size_t n, int d, hipStream_t st) override {
+        return nccl_status(ncclAllToAll(s, r, n, nccl_dtype(d), comm_, st));
+    }
+    int allgather(const void* s, void* r, size_t n, int d, hipStream_t st) override {
+        return nccl_status(ncclAllGather(s, r, n, nccl_dtype(d), comm_, st));
+    }
+    int send(const void* b, size_t n, int d, int peer, hipStream_t st) override {
+        return nccl_status(ncclSend(b, n, nccl_dtype(d), peer, comm_, st));
+    }
+    int recv(void* b, size_t n, int d, int peer, hipStream_t st) override {
+        return nccl_status(ncclRecv(b, n, nccl_dtype(d), peer, comm_, st));
+    }
+    int group_start() override { return nccl_status(ncclGroupStart()); }
+    int group_end() override { return nccl_status(ncclGroupEnd()); }
+    int abort() override {
+        int rc = BAGUA_OK;
+        if (comm_) rc = nccl_status(ncclCommAbort(comm_));
+        comm_ = nullptr;
+        return rc;
+    }
+
+   private:
+    ncclComm_t comm_;
+};
+
+Transport* make_rccl_transport(ncclComm_t comm) { return new RcclTransport(comm); }
+
 }  // namespace bagua
 
 using namespace bagua;
 
-#define COMM_CHECK(c)                                  \
-    do {                                               \
-        if (!(c) || !(c)->comm) return BAGUA_ERR_INVALID_ARG; \
-        if ((c)->aborted.load()) return BAGUA_ERR_ABORTED;    \
+#define COMM_CHECK(c)                                        \
+    do {                                                     \
+        if (!(c) || !(c)->t) return BAGUA_ERR_INVALID_ARG;   \
+        if ((c)->aborted.load()) return BAGUA_ERR_ABORTED;   \
     } while (0)
 
 extern "C" {
@@ -114,15 +153,14 @@ BaguaSingleCommunicatorC* bagua_single_communicator_c_create(size_t rank, size_t
     if (!base64_decode(nccl_unique_id_str, &bytes) || bytes.size() < NCCL_UNIQUE_ID_BYTES) return nullptr;
     ncclUniqueId id;
     std::memcpy(id.internal, bytes.data(), NCCL_UNIQUE_ID_BYTES);
+    ncclComm_t comm = nullptr;
+    if (ncclCommInitRank(&comm, (int)nranks, id, (int)rank) != ncclSuccess) return nullptr;
     auto* c = new BaguaSingleCommunicatorC();
+    c->t = make_rccl_transport(comm);
     c->rank = rank;
     c->nranks = nranks;
     c->device_id = (int)device_id;
     c->stream = (hipStream_t)(uintptr_t)stream_ptr;
-    if (ncclCommInitRank(&c->comm, (int)nranks, id, (int)rank) != ncclSuccess) {
-        delete c;
-        return nullptr;
-    }
     BAGUA_LOG(3, "communicator rank %zu/%zu on device %zu ready", rank, nranks, device_id);
     return c;
 }
@@ -131,10 +169,8 @@ void bagua_single_communicator_c_destroy(BaguaSingleCommunicatorC** ptr) {
     // bagua-core-c/src/lib.rs:32-53: null-safe, nulls the caller's pointer
     if (!ptr || !*ptr) return;
     BaguaSingleCommunicatorC* c = *ptr;
-    if (c->comm) {
-        if (c->aborted.load()) (void)ncclCommAbort(c->comm);
-        else (void)ncclCommDestroy(c->comm);
-    }
+    if (c->t && c->aborted.load()) c->t->abort();
+    delete c->t;
     delete c;
     *ptr = nullptr;
 }
@@ -160,12 +196,7 @@ int bagua_comm_abort(BaguaSingleCommunicatorC* c) {
     // communicators/mod.rs:456-466
     if (!c) return BAGUA_ERR_INVALID_ARG;
     c->aborted.store(true);
-    int rc = BAGUA_OK;
-    if (c->comm) {
-        rc = nccl_status(ncclCommAbort(c->comm));
-        c->comm = nullptr;
-    }
-    return rc;
+    return c->t ? c->t->abort() : BAGUA_OK;
 }
 
 int bagua_comm_check_abort(BaguaSingleCommunicatorC* c) { return c && c->aborted.load() ? 1 : 0; }
@@ -175,21 +206,20 @@ int bagua_comm_allreduce_inplace(BaguaSingleCommunicatorC* c, const bagua_tensor
     COMM_CHECK(c);
     if (!t) return BAGUA_ERR_INVALID_ARG;
     void* p = (void*)(uintptr_t)t->ptr;
-    return nccl_status(ncclAllReduce(p, p, t->num_elem_allocated, nccl_dtype(t->dtype), nccl_op(op), c->comm, c->stream));
+    return c->t->allreduce(p, p, t->num_elem_allocated, t->dtype, op, c->stream);
 }
 
 int bagua_comm_allreduce(BaguaSingleCommunicatorC* c, const bagua_tensor_t* s, const bagua_tensor_t* r, int op) {
     COMM_CHECK(c);
     if (!s || !r || s->dtype != r->dtype || s->num_elem_allocated != r->num_elem_allocated) return BAGUA_ERR_INVALID_ARG;
-    return nccl_status(ncclAllReduce((const void*)(uintptr_t)s->ptr, (void*)(uintptr_t)r->ptr, s->num_elem_allocated,
-                                     nccl_dtype(s->dtype), nccl_op(op), c->comm, c->stream));
+    return c->t->allreduce((const void*)(uintptr_t)s->ptr, (void*)(uintptr_t)r->ptr, s->num_elem_allocated, s->dtype,
+                           op, c->stream);
 }
 
 int bagua_comm_broadcast(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int root) {
     COMM_CHECK(c);
     if (!t) return BAGUA_ERR_INVALID_ARG;
-    void* p = (void*)(uintptr_t)t->ptr;
-    return nccl_status(ncclBroadcast(p, p, t->num_elem_allocated, nccl_dtype(t->dtype), root, c->comm, c->stream));
+    return c->t->broadcast((void*)(uintptr_t)t->ptr, t->num_elem_allocated, t->dtype, root, c->stream);
 }
 
 int bagua_comm_alltoall(BaguaSingleCommunicatorC* c, const bagua_tensor_t* s, const bagua_tensor_t* r) {
@@ -197,9 +227,8 @@ int bagua_comm_alltoall(BaguaSingleCommunicatorC* c, const bagua_tensor_t* s, co
     if (!s || !r || s->dtype != r->dtype || s->num_elem_allocated % c->nranks ||
         r->num_elem_allocated < s->num_elem_allocated)
         return BAGUA_ERR_INVALID_ARG;
-    const size_t count = s->num_elem_allocated / c->nranks;
-    return nccl_status(ncclAllToAll((const void*)(uintptr_t)s->ptr, (void*)(uintptr_t)r->ptr, count,
-                                    nccl_dtype(s->dtype), c->comm, c->stream));
+    return c->t->alltoall((const void*)(uintptr_t)s->ptr, (void*)(uintptr_t)r->ptr, s->num_elem_allocated / c->nranks,
+                          s->dtype, c->stream);
 }
 
 int bagua_comm_alltoall_inplace(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t) {
@@ -227,28 +256,26 @@ int bagua_comm_allgather_inplace(BaguaSingleCommunicatorC* c, const bagua_tensor
     const size_t count = t->num_elem_allocated / c->nranks;
     uint8_t* base = (uint8_t*)(uintptr_t)t->ptr;
     const size_t esz = bagua_dtype_bytes(t->dtype);
-    return nccl_status(ncclAllGather(base + c->rank * count * esz, base, count, nccl_dtype(t->dtype), c->comm, c->stream));
+    return c->t->allgather(base + c->rank * count * esz, base, count, t->dtype, c->stream);
 }
 
 int bagua_comm_allgather(BaguaSingleCommunicatorC* c, const bagua_tensor_t* s, const bagua_tensor_t* r) {
     COMM_CHECK(c);
     if (!s || !r || r->num_elem_allocated != s->num_elem_allocated * c->nranks) return BAGUA_ERR_INVALID_ARG;
-    return nccl_status(ncclAllGather((const void*)(uintptr_t)s->ptr, (void*)(uintptr_t)r->ptr, s->num_elem_allocated,
-                                     nccl_dtype(s->dtype), c->comm, c->stream));
+    return c->t->allgather((const void*)(uintptr_t)s->ptr, (void*)(uintptr_t)r->ptr, s->num_elem_allocated, s->dtype,
+                           c->stream);
 }
 
 int bagua_comm_send(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int peer) {
     COMM_CHECK(c);
     if (!t) return BAGUA_ERR_INVALID_ARG;
-    return nccl_status(ncclSend((const void*)(uintptr_t)t->ptr, t->num_elem_allocated, nccl_dtype(t->dtype), peer,
-                                c->comm, c->stream));
+    return c->t->send((const void*)(uintptr_t)t->ptr, t->num_elem_allocated, t->dtype, peer, c->stream);
 }
 
 int bagua_comm_recv(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int peer) {
     COMM_CHECK(c);
     if (!t) return BAGUA_ERR_INVALID_ARG;
-    return nccl_status(ncclRecv((void*)(uintptr_t)t->ptr, t->num_elem_allocated, nccl_dtype(t->dtype), peer, c->comm,
-                                c->stream));
+    return c->t->recv((void*)(uintptr_t)t->ptr, t->num_elem_allocated, t->dtype, peer, c->stream);
 }
 
 int bagua_comm_group_start(void) { return nccl_status(ncclGroupStart()); }
@@ -266,7 +293,7 @@ int bagua_comm_barrier(BaguaSingleCommunicatorC* c) {
     int rc = b.allocate(c->device_id, 4);
     if (rc) return rc;
     if (hipMemsetAsync(b.as<void>(), 0, 4, c->stream) != hipSuccess) return BAGUA_ERR_HIP;
-    rc = nccl_status(ncclAllReduce(b.as<void>(), b.as<void>(), 1, ncclFloat32, ncclSum, c->comm, c->stream));
+    rc = c->t->allreduce(b.as<void>(), b.as<void>(), 1, BAGUA_DTYPE_F32, BAGUA_OP_SUM, c->stream);
     if (rc) return rc;
     return bagua_comm_synchronize(c);
 }

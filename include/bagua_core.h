@@ -112,6 +112,14 @@ int bagua_comm_group_end(void);
 int bagua_comm_barrier(BaguaSingleCommunicatorC* comm);
 int bagua_comm_synchronize(BaguaSingleCommunicatorC* comm);
 
+/* In-process loopback transport (test harness): nranks virtual ranks, one host
+ * thread each, on one device; collectives are device-to-device copies.  Runs
+ * the comm ops below at nranks > 1 on a single GPU.  Destroy communicators
+ * with bagua_single_communicator_c_destroy, then the group. */
+void* bagua_loopback_group_create(int nranks, int device_id);
+void bagua_loopback_group_destroy(void* group);
+BaguaSingleCommunicatorC* bagua_loopback_communicator_create(void* group, size_t rank, uint64_t stream_ptr);
+
 /* ------------------------------------------------------------- comm ops -- */
 /* CentralizedLowPrecisionSynchronous::execute_background_communication on one
  * flat communication tensor (centralized_low_precision_synchronous.rs:16-73). */

@@ -1,0 +1,131 @@
+"""GPU tests of the comm ops at p > 1 on a single MI355X.
+
+The C++ comm ops (csrc/runtime/comm_ops.cpp) run unchanged on the in-process
+loopback transport: p virtual ranks, one host thread each, on one device,
+collectives as device-to-device copies (csrc/runtime/loopback.cpp).  Every
+rank's result must equal the oracle simulation of the reference op sequence
+bit-for-bit (and, for the centralized op, all ranks must agree)."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle_np as NP
+from oracle import simulate
+
+pytestmark = pytest.mark.gpu
+
+F32, F16, BF16 = 0, 1, 2
+TORCH = {F32: torch.float32, F16: torch.float16, BF16: torch.bfloat16}
+
+
+@pytest.fixture(scope="module")
+def bc():
+    import bagua_core
+    return bagua_core
+
+
+def dev(x, dtype):
+    if dtype == BF16:
+        return torch.from_numpy(x.view(np.int16).copy()).view(torch.bfloat16).cuda()
+    return torch.from_numpy(x.copy()).cuda()
+
+
+def host(t, dtype):
+    torch.cuda.synchronize()
+    if dtype == BF16:
+        return t.view(torch.int16).cpu().numpy().view(np.uint16)
+    return t.cpu().numpy()
+
+
+def run_ranks(fn, p):
+    errs = [None] * p
+    def wrap(r):
+        try:
+            fn(r)
+        except BaseException as e:  # noqa: BLE001
+            errs[r] = e
+    ths = [threading.Thread(target=wrap, args=(r,)) for r in range(p)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=300)
+    for e in errs:
+        if e is not None:
+            raise e
+
+
+@pytest.mark.parametrize("p,dtype,cs,fused", [(2, F32, 40000, True), (4, F32, 65536, True), (8, F32, 12345 * 4, True),
+                                              (8, BF16, 20000, True), (4, F16, 8192, True), (4, F32, 10000, False),
+                                              (3, F32, 3 * 1024, True), (16, F32, 4096, True)])
+def test_centralized_low_precision_multirank(bc, oracle_c, p, dtype, cs, fused):
+    from bagua_core.communicator import loopback_communicators
+    if oracle_c.minmax_compressed_size(p, cs, dtype) % p:
+        pytest.skip("reference alltoall requires S % nranks == 0")
+    rng = np.random.default_rng(p * 100 + dtype)
+    xs = [NP.from_f32((rng.standard_normal(p * cs) * 1e-3 + 0.01 * r).astype(np.float32), dtype) for r in range(p)]
+    want = simulate.centralized_low_precision(oracle_c, xs, dtype, True)
+    comms = loopback_communicators(p, 0)
+    ts = [dev(x, dtype) for x in xs]
+    torch.cuda.synchronize()
+    N = bc._native
+    fn = (N.C.bagua_centralized_low_precision_synchronous if fused
+          else N.C.bagua_centralized_low_precision_synchronous_unfused)
+
+    def rank(r):
+        raw = bc.BaguaTensorPy(ts[r], f"g{r}").raw()
+        N.check(fn(comms[r].handle, ctypes.byref(raw), 1, N.COMPRESSION_MINMAX_UINT8), f"rank {r}")
+
+    run_ranks(rank, p)
+    outs = [host(t, dtype) for t in ts]
+    for r in range(p):
+        assert np.array_equal(outs[r].view(np.uint8), want[r].view(np.uint8)), f"rank {r}"
+        assert np.array_equal(outs[r].view(np.uint8), outs[0].view(np.uint8))
+
+
+@pytest.mark.parametrize("p", [2, 4])
+def test_centralized_onebit_multirank(bc, oracle_c, p):
+    from bagua_core.communicator import loopback_communicators
+    cs = 4096 * 3
+    rng = np.random.default_rng(p)
+    xs = [(rng.standard_normal(p * cs) * 1e-3).astype(np.float32) for _ in range(p)]
+    want = simulate.centralized_low_precision(oracle_c, xs, F32, True, method="OneBitSignScale")
+    comms = loopback_communicators(p, 0)
+    ts = [dev(x, F32) for x in xs]
+    torch.cuda.synchronize()
+    N = bc._native
+
+    def rank(r):
+        raw = bc.BaguaTensorPy(ts[r], "g").raw()
+        N.check(N.C.bagua_centralized_low_precision_synchronous(comms[r].handle, ctypes.byref(raw), 1,
+                                                                N.COMPRESSION_ONEBIT), f"rank {r}")
+
+    run_ranks(rank, p)
+    for r in range(p):
+        assert np.array_equal(host(ts[r], F32).view(np.uint32), want[r].view(np.uint32)), f"rank {r}"
+
+
+@pytest.mark.parametrize("p,dtype", [(2, F32), (3, F32), (4, BF16), (8, F32)])
+def test_decentralized_low_precision_multirank(bc, oracle_c, p, dtype):
+    from bagua_core.communicator import loopback_communicators
+    n = 30011
+    rng = np.random.default_rng(50 + p)
+    arrs = {k: [NP.from_f32((rng.standard_normal(n) * 1e-3).astype(np.float32), dtype) for _ in range(p)]
+            for k in "twlr"}
+    want = simulate.decentralized_low_precision(oracle_c, arrs["t"], arrs["w"], arrs["l"], arrs["r"], dtype)
+    comms = loopback_communicators(p, 0)
+    dts = {k: [dev(a, dtype) for a in arrs[k]] for k in "twlr"}
+    torch.cuda.synchronize()
+    N = bc._native
+
+    def rank(r):
+        raws = [bc.BaguaTensorPy(dts[k][r], k).raw() for k in "twlr"]
+        N.check(N.C.bagua_decentralized_low_precision_synchronous(comms[r].handle, *[ctypes.byref(x) for x in raws],
+                                                                  N.COMPRESSION_MINMAX_UINT8), f"rank {r}")
+
+    run_ranks(rank, p)
+    for k, wk in zip("twlr", want):
+        for r in range(p):
+            assert np.array_equal(host(dts[k][r], dtype).view(np.uint8), wk[r].view(np.uint8)), f"{k} rank {r}"
