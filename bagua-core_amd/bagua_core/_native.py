@@ -65,6 +65,13 @@ KERNEL_SIGNATURES = {
     "bagua_minmax_u8_decompress_reduce": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _vp]),
     "bagua_minmax_u8_reduce_requantize": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _vp, _sz, _i32, _vp, _sz,
                                                  _vp]),
+    "bagua_minmax_u8_piece_range": (_i32, [_i32, _i32, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    "bagua_minmax_u8_pipeline_workspace_bytes": (_sz, [_i32, _i32]),
+    "bagua_minmax_u8_quantize_range": (_i32, [_i32, _vp, _i32, _i32, _i32, _vp, _sz, _vp, _sz, _i32, _i32, _i32,
+                                              _vp]),
+    "bagua_minmax_u8_decompress_range": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _i32, _vp]),
+    "bagua_minmax_u8_reduce_piece": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _sz, _vp]),
+    "bagua_minmax_u8_requantize_pieces": (_i32, [_i32, _vp, _i32, _i32, _vp, _sz, _i32, _i32, _vp, _sz, _vp]),
     "bagua_onebit_compressed_bytes": (_sz, [_i32, _i32]),
     "bagua_onebit_workspace_bytes": (_sz, [_i32, _i32]),
     "bagua_onebit_compress": (_i32, [_i32, _vp, _i32, _i32, _i32, _vp, _sz, _vp, _sz, _i32, _vp]),
@@ -142,6 +149,7 @@ CORE_SIGNATURES = {
     "bagua_loopback_communicator_create": (_C, [_vp, _sz, _u64]),
     "bagua_centralized_low_precision_synchronous": (_i32, [_C, _T, _i32, _i32]),
     "bagua_centralized_low_precision_synchronous_unfused": (_i32, [_C, _T, _i32, _i32]),
+    "bagua_centralized_low_precision_pipelined": (_i32, [_C, _T, _i32, _i32, _i32]),
     "bagua_centralized_full_precision_synchronous": (_i32, [_C, _T, _i32]),
     "bagua_decentralized_low_precision_synchronous": (_i32, [_C, _T, _T, _T, _T, _i32]),
 }

@@ -118,15 +118,19 @@ __global__ __launch_bounds__(kBlock) void minmax_partials_kernel(
 // ------------------------------------------------------------------------
 template <typename T, bool kReverse>
 __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
-    const typename T::storage* __restrict__ in, int64_t in_num_elem, int64_t cs, int target,
-    const uint2* __restrict__ partials, int npartials, uint8_t* __restrict__ out,
+    const typename T::storage* __restrict__ in, int64_t in_num_elem, int64_t cs, int64_t e0, int64_t e1,
+    int target, const uint2* __restrict__ partials, int npartials, uint8_t* __restrict__ out,
     int64_t chunk_offset, int64_t out_bytes, int num_chunks) {
+    // quantises elements [e0, e1) of each chunk (the whole chunk: [0, cs));
+    // the range starting at 0 writes the header, the one ending at cs the slack
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
     const int cidx = kReverse ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
     const int c = target < 0 ? cidx : target;
-    const int64_t n = chunk_valid(in_num_elem, cs, c);
-    const S* src = in + (int64_t)c * cs;
+    const int64_t len = e1 - e0;
+    int64_t n = chunk_valid(in_num_elem, cs, c) - e0;  // valid elements of the range
+    n = n < 0 ? 0 : (n > len ? len : n);
+    const S* src = in + (int64_t)c * cs + e0;
     uint8_t* seg = out + (int64_t)c * chunk_offset;
 
     // fold the chunk's partials (written by pass 1; L2/MALL-resident)
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
     const float mn = from_min_space(lo), mx = from_max_space(hi);
     const QParams q = make_qparams(mn, mx);
 
-    if (blockIdx.x == 0) {
+    if (blockIdx.x == 0 && e0 == 0) {
         // header {T min, T max, zero gap} (reference leaves the gap uninitialised)
         if (threadIdx.x < 32) {
             uint32_t hb = 0;
@@ -159,6 +163,8 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
             else if (t < 2 * (int)sizeof(S)) hb = (bmx >> (8 * (t - (int)sizeof(S)))) & 0xff;
             seg[t] = (uint8_t)hb;
         }
+    }
+    if (blockIdx.x == 0 && e1 == cs) {
         // slack after the payload, and the buffer tail after the last segment
         for (int64_t j = 32 + cs + threadIdx.x; j < chunk_offset; j += kBlock) seg[j] = 0;
         if (target < 0 && c == num_chunks - 1)
@@ -166,19 +172,19 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
                 out[j] = 0;
     }
 
-    uint8_t* payload = seg + 32;
+    uint8_t* payload = seg + 32 + e0;
     const int a = common_alignment<T>((uintptr_t)src, (uintptr_t)payload);
     if (a < 0) {  // no common vector alignment: scalar path over the whole chunk
-        for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < cs; j += (int64_t)gridDim.x * kBlock)
+        for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < len; j += (int64_t)gridDim.x * kBlock)
             payload[j] = (uint8_t)(j < n ? quant(T::to_f(src[j]), q) : 0u);
         return;
     }
-    const int64_t j0 = a < cs ? a : cs;
-    const int64_t nvec = (cs - j0) / N;
+    const int64_t j0 = a < len ? a : len;
+    const int64_t nvec = (len - j0) / N;
     const uint4* __restrict__ vsrc = reinterpret_cast<const uint4*>(src + j0);
     uint8_t* vdst = payload + j0;
     const int64_t ntiles = (nvec + kVecPerBlockTile - 1) / kVecPerBlockTile;
-    const bool all_valid = (n == cs);  // elements past in_num_elem quantise to 0
+    const bool all_valid = (n == len);  // elements past in_num_elem quantise to 0
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int64_t base = (kReverse ? (ntiles - 1 - t) : t) * kVecPerBlockTile;
         if (all_valid && base + kVecPerBlockTile <= nvec) {
@@ -213,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
     if (blockIdx.x == 0) {
         for (int64_t j = threadIdx.x; j < j0; j += kBlock)
             payload[j] = (uint8_t)(j < n ? quant(T::to_f(src[j]), q) : 0u);
-        for (int64_t j = j0 + nvec * N + threadIdx.x; j < cs; j += kBlock)
+        for (int64_t j = j0 + nvec * N + threadIdx.x; j < len; j += kBlock)
             payload[j] = (uint8_t)(j < n ? quant(T::to_f(src[j]), q) : 0u);
     }
 }
@@ -223,24 +229,26 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
 // ------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
-    const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs,
+    const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int64_t e0, int64_t e1,
     typename T::storage* __restrict__ out) {
+    // dequantises elements [e0, e1) of each chunk
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
     const int c = blockIdx.y;
     const uint8_t* seg = in + (int64_t)c * chunk_offset;
     const QParams q = read_header<T>(seg);
-    const uint8_t* payload = seg + 32;
-    S* dst = out + (int64_t)c * cs;
+    const uint8_t* payload = seg + 32 + e0;
+    S* dst = out + (int64_t)c * cs + e0;
+    const int64_t len = e1 - e0;
 
     const int a = common_alignment<T>((uintptr_t)dst, (uintptr_t)payload);
     if (a < 0) {
-        for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < cs; j += (int64_t)gridDim.x * kBlock)
+        for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < len; j += (int64_t)gridDim.x * kBlock)
             dst[j] = T::from_f(dequant(payload[j], q));
         return;
     }
-    const int64_t j0 = a < cs ? a : cs;
-    const int64_t nvec = (cs - j0) / N;
+    const int64_t j0 = a < len ? a : len;
+    const int64_t nvec = (len - j0) / N;
     uint4* __restrict__ vdst = reinterpret_cast<uint4*>(dst + j0);
     const uint8_t* vsrc = payload + j0;
     const int64_t stride = (int64_t)gridDim.x * kVecPerBlockTile;
@@ -276,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
     }
     if (blockIdx.x == 0) {
         for (int64_t j = threadIdx.x; j < j0; j += kBlock) dst[j] = T::from_f(dequant(payload[j], q));
-        for (int64_t j = j0 + nvec * N + threadIdx.x; j < cs; j += kBlock)
+        for (int64_t j = j0 + nvec * N + threadIdx.x; j < len; j += kBlock)
             dst[j] = T::from_f(dequant(payload[j], q));
     }
 }
@@ -300,9 +308,11 @@ static int blocks_for(int64_t elems, int per_vec, int nact, int sub = kSubtiles,
 template <typename T>
 static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint8_t* out,
                          size_t out_bytes, void* ws, size_t ws_bytes, int target, hipStream_t s,
-                         int stages = 3) {
+                         int stages = 3, int e0 = 0, int e1 = -1) {
     using S = typename T::storage;
-    if (p <= 0 || p > 65535 || cs < 0 || target < -1 || target >= p || !input || !out)
+    if (e1 < 0) e1 = cs;
+    if (p <= 0 || p > 65535 || cs < 0 || target < -1 || target >= p || !input || !out || e0 < 0 || e1 < e0 ||
+        e1 > cs)
         return BAGUA_ERR_INVALID_ARG;
     const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);  // K:537
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
@@ -316,9 +326,10 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
         hipLaunchKernelGGL(minmax_partials_kernel<T>, dim3(nblk, nact), dim3(kBlock), 0, s,
                            static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, partials);
     if (stages & 2)
-        hipLaunchKernelGGL((minmax_quantize_kernel<T, true>), dim3(blocks_for(cs, Vec<T>::N, nact), nact),
+        hipLaunchKernelGGL((minmax_quantize_kernel<T, true>), dim3(blocks_for(e1 - e0, Vec<T>::N, nact), nact),
                            dim3(kBlock), 0, s, static_cast<const S*>(input), (int64_t)in_num_elem,
-                           (int64_t)cs, target, partials, nblk, out, chunk_offset, (int64_t)out_bytes, p);
+                           (int64_t)cs, (int64_t)e0, (int64_t)e1, target, partials, nblk, out, chunk_offset,
+                           (int64_t)out_bytes, p);
     return check_launch();
 }
 
@@ -326,7 +337,7 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
 int fused_blocks(int64_t cs, int per_vec);
 template <typename T>
 int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, int average, uint2* partials,
-                        int blocks, hipStream_t s);
+                        int blocks, hipStream_t s, int e0, int e1);
 
 template <typename T>
 static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, void* tensor, int average,
@@ -341,23 +352,73 @@ static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs
     if (!ws || ws_bytes < (size_t)blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
     S* chunk = static_cast<S*>(tensor) + (int64_t)target * cs;
     uint2* partials = static_cast<uint2*>(ws);
-    int rc = dequant_reduce_impl<T>(recv, recv_bytes, cs, p, chunk, average, partials, blocks, s);
+    int rc = dequant_reduce_impl<T>(recv, recv_bytes, cs, p, chunk, average, partials, blocks, s, 0, cs);
     if (rc) return rc;
     hipLaunchKernelGGL((minmax_quantize_kernel<T, true>), dim3(blocks_for(cs, Vec<T>::N, 1), 1), dim3(kBlock), 0, s,
-                       static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, target, partials, blocks, out,
-                       chunk_offset, (int64_t)out_bytes, p);
+                       static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, (int64_t)0, (int64_t)cs, target,
+                       partials, blocks, out, chunk_offset, (int64_t)out_bytes, p);
+    return check_launch();
+}
+
+// ---- pipelined all-reduce building blocks ---------------------------------
+// A chunk is cut into `pieces` element ranges of L = align(ceil(cs/pieces), 512)
+// elements (trailing ones may be empty).  Piece k's fused reduce writes its
+// `fused_blocks(L)` min/max partials to slot k of the workspace; the
+// requantise folds all of them, which is the same min/max as one pass.
+static void piece_range(int cs, int pieces, int k, int* b, int* e) {
+    const int64_t L = (((int64_t)cs + pieces - 1) / pieces + 511) / 512 * 512;
+    const int64_t lo = (int64_t)k * L, hi = lo + L;
+    *b = (int)(lo < cs ? lo : cs);
+    *e = (int)(hi < cs ? hi : cs);
+}
+
+static int piece_blocks(int cs, int pieces, int per_vec) {
+    int b, e;
+    piece_range(cs, pieces, 0, &b, &e);
+    return fused_blocks(e - b, per_vec);
+}
+
+template <typename T>
+static int reduce_piece_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, void* tensor, int average,
+                             int target, int pieces, int piece, void* ws, size_t ws_bytes, hipStream_t s) {
+    using S = typename T::storage;
+    if (p <= 0 || cs < 0 || target < 0 || target >= p || !tensor || pieces < 1 || piece < 0 || piece >= pieces)
+        return BAGUA_ERR_INVALID_ARG;
+    const int blocks = piece_blocks(cs, pieces, Vec<T>::N);
+    if (!ws || ws_bytes < (size_t)pieces * blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
+    int b, e;
+    piece_range(cs, pieces, piece, &b, &e);
+    S* chunk = static_cast<S*>(tensor) + (int64_t)target * cs;
+    return dequant_reduce_impl<T>(recv, recv_bytes, cs, p, chunk, average,
+                                  static_cast<uint2*>(ws) + (size_t)piece * blocks, blocks, s, b, e);
+}
+
+template <typename T>
+static int requantize_pieces_impl(const void* tensor, int cs, int p, uint8_t* out, size_t out_bytes, int target,
+                                  int pieces, const void* ws, size_t ws_bytes, hipStream_t s) {
+    using S = typename T::storage;
+    if (p <= 0 || cs < 0 || target < 0 || target >= p || !tensor || !out || pieces < 1) return BAGUA_ERR_INVALID_ARG;
+    const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);
+    if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
+    const int blocks = piece_blocks(cs, pieces, Vec<T>::N);
+    if (!ws || ws_bytes < (size_t)pieces * blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
+    hipLaunchKernelGGL((minmax_quantize_kernel<T, true>), dim3(blocks_for(cs, Vec<T>::N, 1), 1), dim3(kBlock), 0, s,
+                       static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, (int64_t)0, (int64_t)cs, target,
+                       static_cast<const uint2*>(ws), pieces * blocks, out, chunk_offset, (int64_t)out_bytes, p);
     return check_launch();
 }
 
 template <typename T>
-static int decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, hipStream_t s) {
+static int decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, hipStream_t s,
+                           int e0 = 0, int e1 = -1) {
     using S = typename T::storage;
-    if (p <= 0 || p > 65535 || cs < 0 || !in || !out) return BAGUA_ERR_INVALID_ARG;
+    if (e1 < 0) e1 = cs;
+    if (p <= 0 || p > 65535 || cs < 0 || !in || !out || e0 < 0 || e1 < e0 || e1 > cs) return BAGUA_ERR_INVALID_ARG;
     const int64_t chunk_offset = (int64_t)(in_bytes / (size_t)p);  // K:566
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     hipLaunchKernelGGL(minmax_dequantize_kernel<T>,
-                       dim3(blocks_for(cs, Vec<T>::N, p, kSubtiles, kDequantBlocks), p), dim3(kBlock), 0,
-                       s, in, chunk_offset, (int64_t)cs, static_cast<S*>(out));
+                       dim3(blocks_for(e1 - e0, Vec<T>::N, p, kSubtiles, kDequantBlocks), p), dim3(kBlock), 0,
+                       s, in, chunk_offset, (int64_t)cs, (int64_t)e0, (int64_t)e1, static_cast<S*>(out));
     return check_launch();
 }
 
@@ -445,6 +506,61 @@ int bagua_minmax_u8_reduce_requantize(int dtype, const uint8_t* input, size_t in
     }
     return BAGUA_ERR_UNSUPPORTED;
 }
+
+// ---- pipelined all-reduce building blocks ---------------------------------
+#define BAGUA_DTYPE_DISPATCH(dtype, call)                   \
+    switch (dtype) {                                        \
+        case BAGUA_DTYPE_F32: { using T = F32; return call; } \
+        case BAGUA_DTYPE_F16: { using T = F16; return call; } \
+        case BAGUA_DTYPE_BF16: { using T = BF16; return call; } \
+    }                                                       \
+    return BAGUA_ERR_UNSUPPORTED
+
+int bagua_minmax_u8_piece_range(int chunk_size, int pieces, int piece, int* begin, int* end) {
+    if (chunk_size < 0 || pieces < 1 || piece < 0 || piece >= pieces || !begin || !end) return BAGUA_ERR_INVALID_ARG;
+    piece_range(chunk_size, pieces, piece, begin, end);
+    return BAGUA_OK;
+}
+
+size_t bagua_minmax_u8_pipeline_workspace_bytes(int chunk_size, int pieces) {
+    if (chunk_size < 0 || pieces < 1) return 0;
+    return (size_t)pieces * (size_t)piece_blocks(chunk_size, pieces, 4) * sizeof(uint2) + 256;
+}
+
+int bagua_minmax_u8_quantize_range(int dtype, const void* input, int input_num_element, int chunk_size,
+                                   int num_chunks, uint8_t* output, size_t output_bytes, void* workspace,
+                                   size_t workspace_bytes, int target_chunk, int elem_begin, int elem_end,
+                                   bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    BAGUA_DTYPE_DISPATCH(dtype, compress_impl<T>(input, input_num_element, chunk_size, num_chunks, output,
+                                                 output_bytes, workspace, workspace_bytes, target_chunk, s, 2,
+                                                 elem_begin, elem_end));
+}
+
+int bagua_minmax_u8_decompress_range(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                                     int num_chunks, void* output, int elem_begin, int elem_end,
+                                     bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    BAGUA_DTYPE_DISPATCH(dtype, decompress_impl<T>(input, input_bytes, chunk_size, num_chunks, output, s, elem_begin,
+                                                   elem_end));
+}
+
+int bagua_minmax_u8_reduce_piece(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size, int num_chunks,
+                                 void* tensor, int average, int target_chunk, int pieces, int piece, void* workspace,
+                                 size_t workspace_bytes, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    BAGUA_DTYPE_DISPATCH(dtype, reduce_piece_impl<T>(input, input_bytes, chunk_size, num_chunks, tensor, average,
+                                                     target_chunk, pieces, piece, workspace, workspace_bytes, s));
+}
+
+int bagua_minmax_u8_requantize_pieces(int dtype, const void* tensor, int chunk_size, int num_chunks, uint8_t* output,
+                                      size_t output_bytes, int target_chunk, int pieces, const void* workspace,
+                                      size_t workspace_bytes, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    BAGUA_DTYPE_DISPATCH(dtype, requantize_pieces_impl<T>(tensor, chunk_size, num_chunks, output, output_bytes,
+                                                          target_chunk, pieces, workspace, workspace_bytes, s));
+}
+#undef BAGUA_DTYPE_DISPATCH
 
 // ---- v1 surface (bagua_kernels.cu:661-689) --------------------------------
 void compress_f32_to_uint8_host(float* input, int input_num_element, int chunk_size, int num_chunks,

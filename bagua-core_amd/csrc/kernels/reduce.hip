@@ -137,8 +137,9 @@ static int reduce_impl(void* x, int cs, int p, int target, int average, hipStrea
 // ---------------------------------------------- fused dequantise + reduce --
 template <typename T, int BY, bool AVG, bool PARTIALS>
 __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
-    const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int p,
+    const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t e0, int64_t cs, int p,
     typename T::storage* __restrict__ out, uint2* __restrict__ partials) {
+    // reduces elements [e0, e0 + cs) of the chunk (`out` points at element e0)
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
     __shared__ QParams qp[kMaxFusedChunks];
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
 #pragma unroll
             for (int y = 0; y < BY; ++y) {
                 const int c = r * BY + y;
-                if (c < p) load_bytes<T>(in + (int64_t)c * chunk_offset + 32 + v * N, b[y]);
+                if (c < p) load_bytes<T>(in + (int64_t)c * chunk_offset + 32 + e0 + v * N, b[y]);
             }
 #pragma unroll
             for (int y = 0; y < BY; ++y) {
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
         for (int y = 0; y < BY; ++y) s[y] = 0.0f;
         for (int c = 0; c < p; ++c) {
             const int y = c % BY;
-            s[y] = s[y] + as_stored<T>(dequant(in[(int64_t)c * chunk_offset + 32 + j], qp[c]));
+            s[y] = s[y] + as_stored<T>(dequant(in[(int64_t)c * chunk_offset + 32 + e0 + j], qp[c]));
         }
         tree_finish<BY>(s);
         const S o = T::from_f(AVG ? s[0] / pf : s[0]);
@@ -235,23 +236,23 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
 }
 
 template <typename T, int BY, bool AVG>
-static void launch_fused(const uint8_t* in, int64_t co, int64_t cs, int p, typename T::storage* out,
+static void launch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, int p, typename T::storage* out,
                          uint2* partials, int blocks, hipStream_t s) {
     if (partials)
         hipLaunchKernelGGL((dequant_reduce_kernel<T, BY, AVG, true>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                           cs, p, out, partials);
+                           e0, cs, p, out, partials);
     else
         hipLaunchKernelGGL((dequant_reduce_kernel<T, BY, AVG, false>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                           cs, p, out, partials);
+                           e0, cs, p, out, partials);
 }
 
 template <typename T, bool AVG>
-static void dispatch_fused(const uint8_t* in, int64_t co, int64_t cs, int p, typename T::storage* out,
+static void dispatch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, int p, typename T::storage* out,
                            uint2* partials, int blocks, hipStream_t s) {
     switch (reduce_by(p)) {  // p <= kMaxFusedChunks (16) keeps BY <= 8
-        case 2: launch_fused<T, 2, AVG>(in, co, cs, p, out, partials, blocks, s); break;
-        case 4: launch_fused<T, 4, AVG>(in, co, cs, p, out, partials, blocks, s); break;
-        default: launch_fused<T, 8, AVG>(in, co, cs, p, out, partials, blocks, s); break;
+        case 2: launch_fused<T, 2, AVG>(in, co, e0, cs, p, out, partials, blocks, s); break;
+        case 4: launch_fused<T, 4, AVG>(in, co, e0, cs, p, out, partials, blocks, s); break;
+        default: launch_fused<T, 8, AVG>(in, co, e0, cs, p, out, partials, blocks, s); break;
     }
 }
 
@@ -263,24 +264,26 @@ int fused_blocks(int64_t cs, int per_vec) {
 
 template <typename T>
 int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, int average,
-                        uint2* partials, int blocks, hipStream_t s) {
+                        uint2* partials, int blocks, hipStream_t s, int e0, int e1) {
+    // reduces elements [e0, e1) of the chunk whose element 0 is at `out`
     using S = typename T::storage;
-    if (!in || !out || cs < 0 || p <= 0) return BAGUA_ERR_INVALID_ARG;
+    if (!in || !out || cs < 0 || p <= 0 || e0 < 0 || e1 < e0 || e1 > cs) return BAGUA_ERR_INVALID_ARG;
     if (p > kMaxFusedChunks) return BAGUA_ERR_UNSUPPORTED;  // caller falls back to decompress + reduce
     const int64_t co = (int64_t)(in_bytes / (size_t)p);
     if (co < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     constexpr int N = Vec<T>::N;
     // vector path: out 16-B aligned and every segment payload N-byte aligned
-    const bool aligned = ((uintptr_t)out % 16 == 0) && (((uintptr_t)in + 32) % N == 0) && (co % N == 0);
+    S* o = static_cast<S*>(out) + e0;
+    const bool aligned = ((uintptr_t)o % 16 == 0) && (((uintptr_t)in + 32 + e0) % N == 0) && (co % N == 0);
     if (!aligned) return BAGUA_ERR_UNSUPPORTED;  // caller falls back to decompress + reduce
-    if (average) dispatch_fused<T, true>(in, co, cs, p, static_cast<S*>(out), partials, blocks, s);
-    else dispatch_fused<T, false>(in, co, cs, p, static_cast<S*>(out), partials, blocks, s);
+    if (average) dispatch_fused<T, true>(in, co, e0, e1 - e0, p, o, partials, blocks, s);
+    else dispatch_fused<T, false>(in, co, e0, e1 - e0, p, o, partials, blocks, s);
     return check_launch();
 }
 
-template int dequant_reduce_impl<F32>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t);
-template int dequant_reduce_impl<F16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t);
-template int dequant_reduce_impl<BF16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t);
+template int dequant_reduce_impl<F32>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
+template int dequant_reduce_impl<F16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
+template int dequant_reduce_impl<BF16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
 
 }  // namespace bagua
 
@@ -305,13 +308,13 @@ int bagua_minmax_u8_decompress_reduce(int dtype, const uint8_t* input, size_t in
     switch (dtype) {
         case BAGUA_DTYPE_F32:
             return dequant_reduce_impl<F32>(input, input_bytes, chunk_size, num_chunks, output, average, nullptr,
-                                            fused_blocks(chunk_size, 4), s);
+                                            fused_blocks(chunk_size, 4), s, 0, chunk_size);
         case BAGUA_DTYPE_F16:
             return dequant_reduce_impl<F16>(input, input_bytes, chunk_size, num_chunks, output, average, nullptr,
-                                            fused_blocks(chunk_size, 8), s);
+                                            fused_blocks(chunk_size, 8), s, 0, chunk_size);
         case BAGUA_DTYPE_BF16:
             return dequant_reduce_impl<BF16>(input, input_bytes, chunk_size, num_chunks, output, average, nullptr,
-                                             fused_blocks(chunk_size, 8), s);
+                                             fused_blocks(chunk_size, 8), s, 0, chunk_size);
     }
     return BAGUA_ERR_UNSUPPORTED;
 }

@@ -12,6 +12,7 @@
 
 #include <atomic>
 #include <cstddef>
+#include <vector>
 
 namespace bagua {
 
@@ -44,4 +45,25 @@ struct BaguaSingleCommunicatorC {
     int device_id = 0;
     hipStream_t stream = nullptr;
     std::atomic<bool> aborted{false};
+    // pipelined ops: a second stream for the exchange of piece k while `stream`
+    // runs the codec on piece k+1, and the events that order the two (lazy)
+    hipStream_t side = nullptr;
+    std::vector<hipEvent_t> events;
+
+    int ensure_side(size_t n_events) {
+        if (!side && hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) {
+            side = nullptr;
+            return -1;
+        }
+        while (events.size() < n_events) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -1;
+            events.push_back(e);
+        }
+        return 0;
+    }
+    ~BaguaSingleCommunicatorC() {
+        for (hipEvent_t e : events) (void)hipEventDestroy(e);
+        if (side) (void)hipStreamDestroy(side);
+    }
 };

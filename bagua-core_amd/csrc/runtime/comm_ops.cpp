@@ -25,6 +25,8 @@
 #include "comm_internal.hpp"
 #include "runtime_util.hpp"
 
+#include <cstdlib>
+
 using namespace bagua;
 
 namespace {
@@ -86,7 +88,9 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
     TRY(c->t->alltoall(send.as<void>(), recv.as<void>(), k.S / k.p, BAGUA_DTYPE_U8, c->stream));
     // 3. reduce the p received versions of the own chunk and requantise it into send[rank]
     bool done = false;
-    if (fused && method == BAGUA_COMPRESSION_MINMAX_UINT8) {
+    // the fused kernels treat every allocated element as valid (the reference
+    // compresses num_elements(), datatypes/mod.rs:339): other tensors run unfused
+    if (fused && method == BAGUA_COMPRESSION_MINMAX_UINT8 && t->num_elem == t->num_elem_allocated) {
         const size_t ws_bytes = bagua_minmax_u8_workspace_bytes((int)k.cs, k.p);
         const uint64_t ws = stream_workspace(c->device_id, s, ws_bytes);
         if (!ws) return finish(c, BAGUA_ERR_OOM);
@@ -107,13 +111,175 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
     return finish(c, BAGUA_OK);
 }
 
+// ---- pipelined centralized op ---------------------------------------------
+// The same op as above with each chunk cut into `pieces` element ranges and
+// two streams: the codec runs on the communicator's stream, the exchange of
+// piece k on a side stream while the codec works on piece k+1:
+//
+//   stream: partials | Q0 Q1 .. Qk | R0 R1 .. Rk RQ | D0 D1 .. Dk
+//   side  :             A0 A1 .. Ak            G0 G1 .. Gk
+//   (Q quantise, A alltoall as grouped send/recv, R fused dequantise+reduce,
+//    RQ requantise own chunk, G allgather, D dequantise; each arrow an event)
+//
+// A segment keeps one header per chunk and the pieces are disjoint byte ranges
+// of it, so every buffer holds exactly the bytes of the unpieced op and the
+// result is bit-identical to it (and to the reference sequence).
+int env_int(const char* name, long dflt) {
+    const char* v = std::getenv(name);
+    return v && *v ? (int)std::strtol(v, nullptr, 10) : (int)dflt;
+}
+
+int auto_pieces(size_t cs) {
+    // BAGUA_PIPELINE_PIECES caps the count (1 disables), pieces keep at least
+    // BAGUA_PIPELINE_MIN_PIECE elements (the exchange of a piece is p times that)
+    const int kmax = env_int("BAGUA_PIPELINE_PIECES", 4);
+    const int min_piece = env_int("BAGUA_PIPELINE_MIN_PIECE", 1 << 20);
+    size_t k = cs / (size_t)(min_piece > 0 ? min_piece : 1);
+    if (k > (size_t)kmax) k = (size_t)kmax;
+    return k < 1 ? 1 : (int)k;
+}
+
+bool pipeline_fits(const BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, const Chunking& k) {
+    const size_t esz = bagua_dtype_bytes(t->dtype);
+    const size_t vec = t->dtype == BAGUA_DTYPE_F32 ? 4 : 8;  // payload bytes per 16-B vector
+    return k.p <= 16 && t->num_elem == t->num_elem_allocated && (k.S / k.p) % vec == 0 &&
+           (t->ptr + (uint64_t)k.rank * k.cs * esz) % 16 == 0 && c->t != nullptr;
+}
+
+// bytes [lo, hi) of every segment that piece q covers: the header travels with
+// piece 0, the slack with the last non-empty piece; empty pieces move nothing
+void piece_bytes(const Chunking& k, int pieces, int q, size_t* lo, size_t* hi) {
+    int b = 0, e = 0;
+    bagua_minmax_u8_piece_range((int)k.cs, pieces, q, &b, &e);
+    const size_t co = k.S / k.p;
+    if (q > 0 && b == e) {
+        *lo = *hi = 0;
+        return;
+    }
+    *lo = q == 0 ? 0 : 32 + (size_t)b;
+    *hi = (size_t)e == k.cs ? co : 32 + (size_t)e;
+}
+
+// one piece of the alltoall (send -> recv) or of the in-place allgather (send)
+int exchange_piece(BaguaSingleCommunicatorC* c, const Chunking& k, uint8_t* send, uint8_t* recv, size_t lo,
+                   size_t hi, bool alltoall) {
+    if (hi <= lo) return BAGUA_OK;
+    const size_t co = k.S / k.p, len = hi - lo;
+    hipStream_t s1 = c->side;
+    if (alltoall &&
+        hipMemcpyAsync(recv + k.rank * co + lo, send + k.rank * co + lo, len, hipMemcpyDeviceToDevice, s1) != hipSuccess)
+        return BAGUA_ERR_HIP;
+    if (k.p == 1) return BAGUA_OK;
+    int rc = c->t->group_start();
+    for (int j = 0; j < k.p && !rc; ++j) {
+        if (j == k.rank) continue;
+        if (alltoall) {
+            rc = c->t->send(send + j * co + lo, len, BAGUA_DTYPE_U8, j, s1);
+            if (!rc) rc = c->t->recv(recv + j * co + lo, len, BAGUA_DTYPE_U8, j, s1);
+        } else {
+            rc = c->t->send(send + k.rank * co + lo, len, BAGUA_DTYPE_U8, j, s1);
+            if (!rc) rc = c->t->recv(send + j * co + lo, len, BAGUA_DTYPE_U8, j, s1);
+        }
+    }
+    const int rc_end = c->t->group_end();
+    return rc ? rc : rc_end;
+}
+
+int finish_both(BaguaSingleCommunicatorC* c, int rc) {
+    const hipError_t e1 = hipStreamSynchronize(c->side);
+    const int r0 = finish(c, rc);
+    if (r0) return r0;
+    return e1 == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP;
+}
+
+#define TRY2(x)                          \
+    do {                                 \
+        rc = (x);                        \
+        if (rc) return finish_both(c, rc); \
+    } while (0)
+#define HIP2(x) TRY2((x) == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP)
+
+int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int average, int pieces) {
+    Chunking k;
+    int rc = plan(c, t, BAGUA_COMPRESSION_MINMAX_UINT8, &k);
+    if (rc) return rc;
+    if (pieces < 1) pieces = auto_pieces(k.cs);
+    if (pieces == 1 || !pipeline_fits(c, t, k)) return centralized(c, t, average, BAGUA_COMPRESSION_MINMAX_UINT8, true);
+    DeviceGuard guard(c->device_id);
+    if (c->ensure_side(3 * (size_t)pieces + 1)) return BAGUA_ERR_HIP;
+    hipStream_t s0 = c->stream, s1 = c->side;
+    hipEvent_t* quantised = c->events.data();
+    hipEvent_t* exchanged = quantised + pieces;
+    hipEvent_t* gathered = exchanged + pieces;
+    hipEvent_t requantised = gathered[pieces];
+    const int dt = t->dtype, cs = (int)k.cs, p = k.p;
+    void* x = (void*)(uintptr_t)t->ptr;
+    PoolBuffer send, recv;
+    TRY(send.allocate(c->device_id, k.S));
+    TRY(recv.allocate(c->device_id, k.S));
+    uint8_t* sb = send.as<uint8_t>();
+    uint8_t* rb = recv.as<uint8_t>();
+    size_t ws_bytes = bagua_minmax_u8_workspace_bytes(cs, p);
+    const size_t pws = bagua_minmax_u8_pipeline_workspace_bytes(cs, pieces);
+    if (pws > ws_bytes) ws_bytes = pws;
+    void* ws = (void*)(uintptr_t)stream_workspace(c->device_id, (uint64_t)(uintptr_t)s0, ws_bytes);
+    if (!ws) return finish(c, BAGUA_ERR_OOM);
+    // the side stream starts after everything already queued on the op's stream
+    HIP2(hipEventRecord(requantised, s0));
+    HIP2(hipStreamWaitEvent(s1, requantised, 0));
+    // 1. min/max of every chunk, then quantise + exchange piece by piece
+    TRY2(bagua_minmax_u8_compress_stage(1, dt, x, (int)t->num_elem, cs, p, sb, k.S, ws, ws_bytes, -1, s0));
+    for (int q = 0; q < pieces; ++q) {
+        int b, e;
+        bagua_minmax_u8_piece_range(cs, pieces, q, &b, &e);
+        if (q == 0 || b < e)
+            TRY2(bagua_minmax_u8_quantize_range(dt, x, (int)t->num_elem, cs, p, sb, k.S, ws, ws_bytes, -1, b, e, s0));
+        HIP2(hipEventRecord(quantised[q], s0));
+    }
+    for (int q = 0; q < pieces; ++q) {
+        size_t lo, hi;
+        piece_bytes(k, pieces, q, &lo, &hi);
+        HIP2(hipStreamWaitEvent(s1, quantised[q], 0));
+        TRY2(exchange_piece(c, k, sb, rb, lo, hi, true));
+        HIP2(hipEventRecord(exchanged[q], s1));
+    }
+    // 2. reduce the p received versions of the own chunk piece by piece, requantise it
+    for (int q = 0; q < pieces; ++q) {
+        HIP2(hipStreamWaitEvent(s0, exchanged[q], 0));
+        TRY2(bagua_minmax_u8_reduce_piece(dt, rb, k.S, cs, p, x, average, k.rank, pieces, q, ws, ws_bytes, s0));
+    }
+    TRY2(bagua_minmax_u8_requantize_pieces(dt, x, cs, p, sb, k.S, k.rank, pieces, ws, ws_bytes, s0));
+    HIP2(hipEventRecord(requantised, s0));
+    // 3. allgather + dequantise piece by piece
+    HIP2(hipStreamWaitEvent(s1, requantised, 0));
+    for (int q = 0; q < pieces; ++q) {
+        size_t lo, hi;
+        piece_bytes(k, pieces, q, &lo, &hi);
+        TRY2(exchange_piece(c, k, sb, rb, lo, hi, false));
+        HIP2(hipEventRecord(gathered[q], s1));
+    }
+    for (int q = 0; q < pieces; ++q) {
+        int b, e;
+        bagua_minmax_u8_piece_range(cs, pieces, q, &b, &e);
+        HIP2(hipStreamWaitEvent(s0, gathered[q], 0));
+        if (b < e) TRY2(bagua_minmax_u8_decompress_range(dt, sb, k.S, cs, p, x, b, e, s0));
+    }
+    return finish_both(c, BAGUA_OK);
+}
+
 }  // namespace
 
 extern "C" {
 
+int bagua_centralized_low_precision_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int average,
+                                              int method, int pieces) {
+    if (method != BAGUA_COMPRESSION_MINMAX_UINT8) return centralized(c, t, average, method, true);
+    return centralized_pipelined(c, t, average, pieces);
+}
+
 int bagua_centralized_low_precision_synchronous(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int average,
                                                 int method) {
-    return centralized(c, t, average, method, true);
+    return bagua_centralized_low_precision_pipelined(c, t, average, method, 0);
 }
 
 int bagua_centralized_low_precision_synchronous_unfused(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t,

@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=["auto", "codec", "allreduce", "onebit"], default="auto")
     ap.add_argument("--elements", type=int, default=0, help="override bucket elements")
+    ap.add_argument("--pieces", type=int, default=0,
+                    help="pipelined all-reduce pieces per chunk (0 = automatic, 1 = unpieced)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the cpu_baseline leg")
     return ap.parse_args()
@@ -219,9 +221,10 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     torch.cuda.synchronize()
     raw = BaguaTensorPy(x, "gradient_bucket").raw()
 
-    def compressed_step():
-        N.check(N.C.bagua_centralized_low_precision_synchronous(comm.handle, ctypes.byref(raw), 1,
-                                                                N.COMPRESSION_MINMAX_UINT8), "compressed allreduce")
+    def compressed_step(pieces=args.pieces):
+        N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
+                                                              N.COMPRESSION_MINMAX_UINT8, pieces),
+                "compressed allreduce")
 
     def fp32_step():
         N.check(N.C.bagua_centralized_full_precision_synchronous(comm.handle, ctypes.byref(raw), 1), "fp32 allreduce")
@@ -246,6 +249,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         return float(t.item()) / steps
 
     t_c = timed(compressed_step, args.steps, args.warmup)
+    t_u = timed(lambda: compressed_step(1), max(3, args.steps // 2), max(1, args.warmup // 2))
     t_f = timed(fp32_step, max(3, args.steps // 2), max(1, args.warmup // 2))
     value = world * 4.0 * n / t_c / GiB
     per_rank = 4.0 * n / t_c / GiB
@@ -287,6 +291,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
            "config_index": 4}
     extra = {"per_rank_gib_s": round(per_rank, 2), "fp32_allreduce_gib_s": round(fp32, 2),
              "ratio_vs_fp32": round(per_rank / fp32, 3), "fp32_ms_per_step": round(t_f * 1e3, 3),
+             "pieces": args.pieces or "auto", "unpieced_ms_per_step": round(t_u * 1e3, 3),
              "per_kernel_us": {nm: round(t * 1e3, 2) for nm, t in zip(names, per)}}
     del comm
     return value, t_c * 1e3, roof, cfg, extra

@@ -125,6 +125,14 @@ BaguaSingleCommunicatorC* bagua_loopback_communicator_create(void* group, size_t
  * flat communication tensor (centralized_low_precision_synchronous.rs:16-73). */
 int bagua_centralized_low_precision_synchronous(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,
                                                 int average, int method);
+/* The same op with each chunk cut into `pieces` element ranges, the exchange of
+ * one piece (side stream, grouped send/recv) overlapping the codec kernels of
+ * the next; bit-identical to the unpieced op.  pieces = 0 picks automatically
+ * (BAGUA_PIPELINE_PIECES cap, default 4; BAGUA_PIPELINE_MIN_PIECE elements per
+ * piece, default 1 Mi), 1 disables; the op above runs this with pieces = 0.
+ * MinMaxUInt8 only; shapes the fused kernels cannot take run unpieced. */
+int bagua_centralized_low_precision_pipelined(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t, int average,
+                                              int method, int pieces);
 /* the reference's unfused sequence, kept for A/B measurement and parity */
 int bagua_centralized_low_precision_synchronous_unfused(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,
                                                         int average, int method);

@@ -110,6 +110,34 @@ int bagua_minmax_u8_reduce_requantize(int dtype, const uint8_t* input, size_t in
                                       size_t output_bytes, int target_chunk, void* workspace,
                                       size_t workspace_bytes, bagua_stream_t stream);
 
+/* Pipelined all-reduce building blocks (no reference counterpart: the same
+ * kernels restricted to part of every chunk, so communication of one piece
+ * overlaps the codec work of the next).  A chunk splits into `pieces` element
+ * ranges (bagua_minmax_u8_piece_range; trailing ranges may be empty).  Each
+ * segment keeps ONE header for the whole chunk, so the pieced sequence writes
+ * exactly the bytes of the unpieced one:
+ *   stage 1 of bagua_minmax_u8_compress_stage (all chunks), then
+ *   bagua_minmax_u8_quantize_range per piece (the range at 0 writes headers);
+ *   bagua_minmax_u8_reduce_piece per piece (fused dequantise + reduce of the
+ *   target chunk; min/max partials to the piece's workspace slot), then
+ *   bagua_minmax_u8_requantize_pieces (folds every slot);
+ *   bagua_minmax_u8_decompress_range per piece (needs the headers present). */
+int bagua_minmax_u8_piece_range(int chunk_size, int pieces, int piece, int* begin, int* end);
+size_t bagua_minmax_u8_pipeline_workspace_bytes(int chunk_size, int pieces);
+int bagua_minmax_u8_quantize_range(int dtype, const void* input, int input_num_element, int chunk_size,
+                                   int num_chunks, uint8_t* output, size_t output_bytes, void* workspace,
+                                   size_t workspace_bytes, int target_chunk, int elem_begin, int elem_end,
+                                   bagua_stream_t stream);
+int bagua_minmax_u8_decompress_range(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                                     int num_chunks, void* output, int elem_begin, int elem_end,
+                                     bagua_stream_t stream);
+int bagua_minmax_u8_reduce_piece(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size, int num_chunks,
+                                 void* tensor, int average, int target_chunk, int pieces, int piece, void* workspace,
+                                 size_t workspace_bytes, bagua_stream_t stream);
+int bagua_minmax_u8_requantize_pieces(int dtype, const void* tensor, int chunk_size, int num_chunks, uint8_t* output,
+                                      size_t output_bytes, int target_chunk, int pieces, const void* workspace,
+                                      size_t workspace_bytes, bagua_stream_t stream);
+
 /* K:196-266 elementwise kernels, dtype-generic (f32, f16, bf16) */
 int bagua_add_inplace(int dtype, void* x, const void* y, int n, bagua_stream_t stream);
 int bagua_addmul_inplace(int dtype, void* x, const void* y, int n, float factor, bagua_stream_t stream);

@@ -96,3 +96,21 @@ def test_python_surface_rejects_cpu_and_bad_dtypes(built):
         bagua_core.BaguaTensorPy(torch.zeros(4, dtype=torch.float64, device="cpu"), "x")
     with pytest.raises(RuntimeError):
         bagua_core.BaguaTensorPy(torch.zeros(4), "cpu tensor")  # datatypes/mod.rs:629-633
+
+
+def test_piece_ranges_cover_chunk(built):
+    """bagua_minmax_u8_piece_range (host-only): pieces tile [0, cs) in order, 512-element aligned."""
+    lib = ctypes.CDLL(os.path.join(LIB, "libbagua_kernels.so"))
+    f = lib.bagua_minmax_u8_piece_range
+    f.restype = ctypes.c_int
+    b, e = ctypes.c_int(), ctypes.c_int()
+    for cs, pieces in [(0, 1), (1, 4), (1536, 4), (40000, 3), (1 << 25, 4), (12345, 7)]:
+        pos = 0
+        for q in range(pieces):
+            assert f(cs, pieces, q, ctypes.byref(b), ctypes.byref(e)) == 0
+            assert b.value == pos and e.value >= b.value
+            assert b.value % 512 == 0 or b.value == cs
+            pos = e.value
+        assert pos == cs
+    assert f(10, 0, 0, ctypes.byref(b), ctypes.byref(e)) != 0
+    assert f(10, 2, 2, ctypes.byref(b), ctypes.byref(e)) != 0

@@ -132,6 +132,42 @@ def test_v1_abi_compress_decompress(bc, oracle_c):
     assert_float_bits_equal(to_host(dec, F32), dw, F32, "v1 decode")
 
 
+@pytest.mark.parametrize("dtype,p,cs,pieces,offset", [(F32, 4, 65536 + 77, 3, 0), (BF16, 3, 40000, 4, 1),
+                                                      (F16, 2, 1536, 4, 0), (F32, 1, 5000, 7, 2)])
+def test_minmax_piecewise_building_blocks(bc, oracle_c, dtype, p, cs, pieces, offset):
+    """stage-1 partials + quantize_range per piece == one compress; decompress_range per piece == one decode."""
+    from oracle import oracle_np as NP
+    K = bc._native.K
+    rng = np.random.default_rng(cs + pieces)
+    x = NP.from_f32((rng.standard_normal(p * cs) * 1e-2 + 0.3).astype(np.float32), dtype)
+    want = oracle_c.compress_minmax_u8(x, dtype, p)
+    xt = to_dev(x, dtype, offset)
+    S = K.bagua_minmax_u8_compressed_bytes(dtype, cs, p)
+    out = torch.full((S,), 0xAB, dtype=torch.uint8, device="cuda")
+    wsb = K.bagua_minmax_u8_workspace_bytes(cs, p)
+    ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+    N = bc._native
+    N.check(K.bagua_minmax_u8_compress_stage(1, dtype, xt.data_ptr(), x.size, cs, p, out.data_ptr(), S,
+                                             ws.data_ptr(), wsb, -1, None), "stage 1")
+    b, e = ctypes.c_int(), ctypes.c_int()
+    ranges = []
+    for q in range(pieces):
+        N.check(K.bagua_minmax_u8_piece_range(cs, pieces, q, ctypes.byref(b), ctypes.byref(e)), "range")
+        ranges.append((b.value, e.value))
+    for q in reversed(range(pieces)):  # any order: pieces are disjoint
+        N.check(K.bagua_minmax_u8_quantize_range(dtype, xt.data_ptr(), x.size, cs, p, out.data_ptr(), S, ws.data_ptr(),
+                                                 wsb, -1, ranges[q][0], ranges[q][1], None), f"piece {q}")
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), want)
+    dec_want = np.zeros_like(x)
+    oracle_c.decompress_minmax_u8(want, p, dec_want, dtype)
+    dec = to_dev(np.zeros_like(x), dtype, offset)
+    for q in range(pieces):
+        N.check(K.bagua_minmax_u8_decompress_range(dtype, out.data_ptr(), S, cs, p, dec.data_ptr(), ranges[q][0],
+                                                   ranges[q][1], None), f"decode piece {q}")
+    assert_float_bits_equal(to_host(dec, dtype), dec_want, dtype, "piecewise decode")
+
+
 def test_invalid_arguments_are_reported(bc):
     t = bc.BaguaTensorPy(torch.zeros(10, device="cuda"), "x")
     with pytest.raises(RuntimeError):

@@ -85,6 +85,34 @@ def test_centralized_low_precision_multirank(bc, oracle_c, p, dtype, cs, fused):
         assert np.array_equal(outs[r].view(np.uint8), outs[0].view(np.uint8))
 
 
+@pytest.mark.parametrize("p,dtype,cs,pieces", [(2, F32, 40000, 3), (4, F32, 65536, 4), (8, F32, 12345 * 4, 2),
+                                               (8, BF16, 20000, 5), (4, F16, 8192, 2), (4, F32, 1536, 4),
+                                               (1, F32, 70000, 3), (16, F32, 4096 * 3, 3), (3, F32, 3 * 1024, 4),
+                                               (2, F32, (1 << 21) + 1024, 0)])
+def test_centralized_pipelined_multirank(bc, oracle_c, p, dtype, cs, pieces):
+    """Pieced op (side-stream exchange per piece) == the reference sequence, bit-for-bit.
+    (4, F32, 1536, 4) has an empty trailing piece (pieces are 512-element aligned)."""
+    from bagua_core.communicator import loopback_communicators
+    if oracle_c.minmax_compressed_size(p, cs, dtype) % p:
+        pytest.skip("reference alltoall requires S % nranks == 0")
+    rng = np.random.default_rng(p * 1000 + dtype + cs)
+    xs = [NP.from_f32((rng.standard_normal(p * cs) * 1e-3 - 0.02 * r).astype(np.float32), dtype) for r in range(p)]
+    want = simulate.centralized_low_precision(oracle_c, xs, dtype, True)
+    comms = loopback_communicators(p, 0)
+    ts = [dev(x, dtype) for x in xs]
+    torch.cuda.synchronize()
+    N = bc._native
+
+    def rank(r):
+        raw = bc.BaguaTensorPy(ts[r], f"g{r}").raw()
+        N.check(N.C.bagua_centralized_low_precision_pipelined(comms[r].handle, ctypes.byref(raw), 1,
+                                                              N.COMPRESSION_MINMAX_UINT8, pieces), f"rank {r}")
+
+    run_ranks(rank, p)
+    for r in range(p):
+        assert np.array_equal(host(ts[r], dtype).view(np.uint8), want[r].view(np.uint8)), f"rank {r}"
+
+
 @pytest.mark.parametrize("p", [2, 4])
 def test_centralized_onebit_multirank(bc, oracle_c, p):
     from bagua_core.communicator import loopback_communicators
