@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["auto", "codec", "allreduce", "onebit"], default="auto")
+    ap.add_argument("--workload", choices=["auto", "codec", "allreduce", "onebit", "host"], default="auto")
     ap.add_argument("--elements", type=int, default=0, help="override bucket elements")
     ap.add_argument("--pieces", type=int, default=0,
                     help="pipelined all-reduce pieces per chunk (0 = automatic, 1 = unpieced)")
@@ -173,6 +173,96 @@ def bench_codec(args, onebit: bool = False):
            f"_encode_decode_{4 * n >> 20}MiB_fp32_bucket", "bucket_elements": n, "n_chunks": p,
            "compressed_bytes": S, "config_index": 3 if onebit else 2}
     return value, ms, roof, cfg, extra, x
+
+
+def bench_host(args):
+    """Host-resident rate: the bucket starts and ends in pinned
+    host memory — H2D fp32 -> encode -> decode -> D2H fp32.  `serial` runs the
+    four steps back to back per bucket; `overlapped` keeps two buckets in
+    flight on three streams (H2D of bucket i+1 and D2H of bucket i-1 overlap
+    the codec of bucket i), the steady state of a stream of buckets."""
+    from bagua_core import _native as N
+    K = N.K
+    n = args.elements or (1 << 26)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    g = torch.Generator().manual_seed(0x5EED)
+    src = (torch.randn(n, generator=g) * 1e-3).pin_memory()
+    dst = [torch.empty(n, pin_memory=True) for _ in range(2)]
+    x = [torch.empty(n, device=dev) for _ in range(2)]
+    y = [torch.empty(n, device=dev) for _ in range(2)]
+    S = K.bagua_minmax_u8_compressed_bytes(0, n, 1)
+    wsb = K.bagua_minmax_u8_workspace_bytes(n, 1)
+    comp = [torch.empty(S, dtype=torch.uint8, device=dev) for _ in range(2)]
+    ws = [torch.empty(wsb, dtype=torch.uint8, device=dev) for _ in range(2)]
+    s_in, s_cmp, s_out = (torch.cuda.Stream(device=dev) for _ in range(3))
+
+    def codec(b, st):
+        sp = ctypes.c_void_p(st.cuda_stream)
+        N.check(K.bagua_minmax_u8_compress(0, x[b].data_ptr(), n, n, 1, comp[b].data_ptr(), S, ws[b].data_ptr(), wsb,
+                                           -1, sp), "compress")
+        N.check(K.bagua_minmax_u8_decompress(0, comp[b].data_ptr(), S, n, 1, y[b].data_ptr(), sp), "decompress")
+
+    def serial(steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            with torch.cuda.stream(s_cmp):
+                x[0].copy_(src, non_blocking=True)
+                codec(0, s_cmp)
+                dst[0].copy_(y[0], non_blocking=True)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps
+
+    ev_in = [torch.cuda.Event() for _ in range(2)]
+    ev_cmp = [torch.cuda.Event() for _ in range(2)]
+    ev_out = [torch.cuda.Event() for _ in range(2)]
+
+    def overlapped(steps):
+        torch.cuda.synchronize()
+        for b in range(2):  # start with every buffer free
+            ev_cmp[b].record(s_cmp)
+            ev_out[b].record(s_out)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            b = i % 2
+            s_in.wait_event(ev_cmp[b])       # x[b] consumed by the codec of bucket i-2
+            with torch.cuda.stream(s_in):
+                x[b].copy_(src, non_blocking=True)
+            ev_in[b].record(s_in)
+            s_cmp.wait_event(ev_in[b])
+            s_cmp.wait_event(ev_out[b])      # y[b] drained by the D2H of bucket i-2
+            codec(b, s_cmp)
+            ev_cmp[b].record(s_cmp)
+            s_out.wait_event(ev_cmp[b])
+            with torch.cuda.stream(s_out):
+                dst[b].copy_(y[b], non_blocking=True)
+            ev_out[b].record(s_out)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps
+
+    def copy_rate(to_dev: bool, steps: int):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s_in):
+            for _ in range(steps):
+                (x[0].copy_(src, non_blocking=True) if to_dev else dst[0].copy_(y[0], non_blocking=True))
+        torch.cuda.synchronize()
+        return 4.0 * n / ((time.perf_counter() - t0) / steps) / GiB
+
+    serial(max(1, args.warmup))
+    overlapped(max(2, args.warmup))
+    t_ser = serial(args.steps)
+    t_ovl = overlapped(args.steps)
+    torch.cuda.synchronize()
+    ok = torch.equal(dst[(args.steps - 1) % 2], y[(args.steps - 1) % 2].cpu())
+    value = 4.0 * n / t_ovl / GiB
+    cfg = {"workload": f"minmax_uint8_encode_decode_{4 * n >> 20}MiB_fp32_bucket_host_resident", "bucket_elements": n,
+           "n_chunks": 1, "config_index": 2, "buffers": "pinned host fp32 in/out"}
+    extra = {"serial_gib_s": round(4.0 * n / t_ser / GiB, 2), "serial_ms_per_bucket": round(t_ser * 1e3, 3),
+             "overlapped_gib_s": round(value, 2), "h2d_gib_s": round(copy_rate(True, 5), 2),
+             "d2h_gib_s": round(copy_rate(False, 5), 2), "result_copied_back_intact": bool(ok)}
+    return value, t_ovl * 1e3, None, cfg, extra
 
 
 def cpu_baseline(args, sample_elems: int = 1 << 24):
@@ -311,6 +401,9 @@ def main():
         if rank == 0 and world == 1 and not args.no_cpu_baseline and workload == "codec":
             cpu = cpu_baseline(args)
         dtype = "f32 -> u8" if workload == "codec" else "f32 -> 1bit"
+    elif workload == "host":
+        value, ms, roof, cfg, extra = bench_host(args)
+        dtype = "f32 -> u8"
     else:
         value, ms, roof, cfg, extra = bench_allreduce(args, world, rank, local_rank)
         dtype = "f32 -> u8"
@@ -318,7 +411,8 @@ def main():
         line = {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": dtype,
-                "data": "synthetic fp32 gradients N(0, 1e-3^2) (torch.randn, seed 0x5EED + rank), resident in HBM",
+                "data": "synthetic fp32 gradients N(0, 1e-3^2) (torch.randn, seed 0x5EED + rank), " +
+                        ("in pinned host memory (H2D + D2H timed)" if workload == "host" else "resident in HBM"),
                 "config": cfg, "roofline": roof, "cpu_baseline": cpu}
         line.update(extra)
         print(json.dumps(line), flush=True)
