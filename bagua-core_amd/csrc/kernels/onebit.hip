@@ -147,12 +147,41 @@ __global__ __launch_bounds__(kObFinalizeThreads) void onebit_finalize_kernel(
     const int lane = lane_id(), wave = threadIdx.x / kWave, nw = kObFinalizeThreads / kWave;
     float total = 0.0f;
     if (m1 > 0) {
-        // level 1 -> 2 from global memory
+        // level 1 -> 2 from global memory: each wave takes kFinBatch groups at
+        // once and issues all their loads (clamped, unconditional) before any
+        // tree, so the pass costs one memory latency instead of one per group
         int64_t m = m1;
         const int64_t g1 = (m + kObTile - 1) / kObTile;
-        for (int64_t g = wave; g < g1; g += nw) {
-            const float s = tile_from(part, g * kObTile, m, lane);
-            if (lane == 0) lvl[0][g] = s;
+        constexpr int kFinBatch = 4;
+        for (int64_t g0 = wave; g0 < g1; g0 += (int64_t)nw * kFinBatch) {
+            float a[kFinBatch][4][4];
+            if ((g0 + (int64_t)(kFinBatch - 1) * nw + 1) * kObTile <= m) {
+                // every group of the batch is full: one base per group, immediate offsets
+#pragma unroll
+                for (int j = 0; j < kFinBatch; ++j) {
+                    const float* pj = part + (g0 + (int64_t)j * nw) * kObTile + lane * 4;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) a[j][k][e] = pj[k * 256 + e];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < kFinBatch; ++j)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int64_t r = (g0 + (int64_t)j * nw) * kObTile + k * 256 + lane * 4 + e;
+                            a[j][k][e] = r < m ? part[r] : 0.0f;
+                        }
+            }
+#pragma unroll
+            for (int j = 0; j < kFinBatch; ++j) {
+                const int64_t g = g0 + (int64_t)j * nw;
+                const float s = wave_tree_sum(lane_tree(a[j]));
+                if (lane == 0 && g < g1) lvl[0][g] = s;
+            }
         }
         __syncthreads();
         int cur = 0;
@@ -206,6 +235,7 @@ __global__ __launch_bounds__(kBlock) void onebit_decode_kernel(const uint8_t* __
     const int64_t tiles = (cs + kObTile - 1) / kObTile;
     const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    // (scalar loads of the tile words were tried: 2.4x slower, s_load latency serialises each wave)
     for (int64_t t = wave; t < tiles; t += nwaves) {
         const uint32_t mine = lane < 32 ? reinterpret_cast<const uint32_t*>(bits + t * kObTileBytes)[lane] : 0u;
 #pragma unroll
