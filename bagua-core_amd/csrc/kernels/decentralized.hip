@@ -1,0 +1,225 @@
+// decentralized.hip — the elementwise steps of the decentralized low-precision
+// ring op (decentralized_low_precision_synchronous.rs:42-152) fused into two
+// streaming kernels around the (unchanged) MinMax quantise pass.
+//
+// Reference sequence on one bucket (n elements of T), each step a full pass:
+//   t += L*(1/3); t += R*(1/3); t += W*(-5/3)          :45-60  3 x addmul
+//   compress(t, n_chunks = 1)                           :61-64  min/max + quantise
+//   ... ring exchange of the compressed bytes ...
+//   t = dq(from_left);  L += t                          :126-133
+//   t = dq(from_right); R += t                          :134-141
+//   t = dq(mine);       t += W;  W = t                  :142-151
+// Bytes moved (bf16, N elements of 2 B): 18N + 5N + 31N = 54N.  Fused:
+//   ring_mix   : the three addmuls in registers + the min/max partials of the
+//                result (the quantise pass folds them as its own)        10N
+//   quantise   : minmax_quantize_kernel, unchanged                        3N
+//   ring_apply : the three dequantise+adds and the clone in one pass     17N
+// Every intermediate is rounded to T exactly where the reference stores it
+// (as_stored<T>), so all four tensors end bit-identical to the reference op.
+#include "codec_common.hpp"
+#include "launch_util.hpp"
+
+namespace bagua {
+
+int minmax_partials_blocks(int64_t cs, int per_vec, int nact, size_t ws_bytes);  // minmax_u8.hip
+
+// K:236-244 addmul as the elementwise kernels compute it (elementwise.hip)
+template <typename T>
+__device__ __forceinline__ float addmul(float x, float y, float f) {
+    if constexpr (sizeof(typename T::storage) == 4) return __builtin_fmaf(y, f, x);
+    else return as_stored<T>(x + as_stored<T>(y * f));
+}
+
+template <typename T>
+__device__ __forceinline__ float mix(float t, float l, float r, float w, float f13, float f53) {
+    t = as_stored<T>(addmul<T>(t, l, f13));
+    t = as_stored<T>(addmul<T>(t, r, f13));
+    return as_stored<T>(addmul<T>(t, w, f53));
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* __restrict__ t,
+                                                          const typename T::storage* __restrict__ l,
+                                                          const typename T::storage* __restrict__ r,
+                                                          const typename T::storage* __restrict__ w, int64_t n,
+                                                          float f13, float f53, uint2* __restrict__ partials) {
+    constexpr int N = Vec<T>::N;
+    uint32_t lo = min_space(T::init_max()), hi = max_space(-T::init_max());
+    const int64_t nvec = n / N;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nvec; v += stride) {
+        const uint4 rt = reinterpret_cast<const uint4*>(t)[v];
+        const uint4 rl = nt_load16(reinterpret_cast<const uint4*>(l) + v);
+        const uint4 rr = nt_load16(reinterpret_cast<const uint4*>(r) + v);
+        const uint4 rw = reinterpret_cast<const uint4*>(w)[v];
+        float ft[N], fl[N], fr[N], fw[N];
+        unpack16<T>(rt, ft);
+        unpack16<T>(rl, fl);
+        unpack16<T>(rr, fr);
+        unpack16<T>(rw, fw);
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            ft[i] = mix<T>(ft[i], fl[i], fr[i], fw[i], f13, f53);
+            const int32_t k = f2key(ft[i]);  // NaN wraps to a huge key in both spaces
+            lo = min(lo, min_space_key(k));
+            hi = min(hi, max_space_key(k));
+        }
+        // plain store: the quantise pass re-reads t next
+        reinterpret_cast<uint4*>(t)[v] = pack16<T>(ft);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < n - nvec * N) {  // ragged tail
+        const int64_t j = nvec * N + threadIdx.x;
+        const float x = mix<T>(T::to_f(t[j]), T::to_f(l[j]), T::to_f(r[j]), T::to_f(w[j]), f13, f53);
+        t[j] = T::from_f(x);
+        const int32_t k = f2key(x);
+        lo = min(lo, min_space_key(k));
+        hi = min(hi, max_space_key(k));
+    }
+    lo = wave_umin(lo);
+    hi = wave_umin(hi);
+    __shared__ uint32_t red[2][kWavesPerBlock];
+    const int wv = threadIdx.x / kWave;
+    if (lane_id() == 0) { red[0][wv] = lo; red[1][wv] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 1; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
+        partials[blockIdx.x] = make_uint2(lo, hi);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __restrict__ mine,
+                                                            const uint8_t* __restrict__ from_left,
+                                                            const uint8_t* __restrict__ from_right,
+                                                            typename T::storage* __restrict__ t,
+                                                            typename T::storage* __restrict__ w,
+                                                            typename T::storage* __restrict__ l,
+                                                            typename T::storage* __restrict__ r, int64_t n) {
+    constexpr int N = Vec<T>::N;
+    const QParams qm = read_header<T>(mine), ql = read_header<T>(from_left), qr = read_header<T>(from_right);
+    const uint8_t* pm = mine + 32;
+    const uint8_t* pl = from_left + 32;
+    const uint8_t* pr = from_right + 32;
+    const int64_t nvec = n / N;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nvec; v += stride) {
+        uint32_t bm[N], bl[N], br[N];
+        load_bytes<T>(pm + v * N, bm);
+        load_bytes<T>(pl + v * N, bl);
+        load_bytes<T>(pr + v * N, br);
+        const uint4 rl = reinterpret_cast<const uint4*>(l)[v];
+        const uint4 rr = reinterpret_cast<const uint4*>(r)[v];
+        const uint4 rw = reinterpret_cast<const uint4*>(w)[v];
+        float fl[N], fr[N], fw[N], ft[N];
+        unpack16<T>(rl, fl);
+        unpack16<T>(rr, fr);
+        unpack16<T>(rw, fw);
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            fl[i] = fl[i] + as_stored<T>(dequant(bl[i], ql));   // L += dq(from_left)
+            fr[i] = fr[i] + as_stored<T>(dequant(br[i], qr));   // R += dq(from_right)
+            ft[i] = as_stored<T>(dequant(bm[i], qm)) + fw[i];   // t = dq(mine) + W
+        }
+        const uint4 ot = pack16<T>(ft);
+        nt_store16(pack16<T>(fl), reinterpret_cast<uint4*>(l) + v);
+        nt_store16(pack16<T>(fr), reinterpret_cast<uint4*>(r) + v);
+        nt_store16(ot, reinterpret_cast<uint4*>(t) + v);
+        nt_store16(ot, reinterpret_cast<uint4*>(w) + v);         // W = t (clone)
+    }
+    if (blockIdx.x == 0 && threadIdx.x < n - nvec * N) {
+        const int64_t j = nvec * N + threadIdx.x;
+        l[j] = T::from_f(T::to_f(l[j]) + as_stored<T>(dequant(pl[j], ql)));
+        r[j] = T::from_f(T::to_f(r[j]) + as_stored<T>(dequant(pr[j], qr)));
+        const typename T::storage o = T::from_f(as_stored<T>(dequant(pm[j], qm)) + T::to_f(w[j]));
+        t[j] = o;
+        w[j] = o;
+    }
+}
+
+static float round_to_t(int dtype, float f) {
+    if (dtype == BAGUA_DTYPE_F16) return (float)(_Float16)f;
+    if (dtype == BAGUA_DTYPE_BF16) {
+        uint32_t u = __builtin_bit_cast(uint32_t, f);
+        if ((u & 0x7fffffffu) > 0x7f800000u) return f;
+        u += 0x7fffu + ((u >> 16) & 1u);
+        return __builtin_bit_cast(float, u & 0xffff0000u);
+    }
+    return f;
+}
+
+static bool aligned16(const void* p) { return (uintptr_t)p % 16 == 0; }
+
+template <typename T>
+static int mix_impl(void* t, const void* l, const void* r, const void* w, int n, void* ws, size_t ws_bytes,
+                    float f13, float f53, hipStream_t s) {
+    using S = typename T::storage;
+    if (!t || !l || !r || !w || n < 0) return BAGUA_ERR_INVALID_ARG;
+    if (!aligned16(t) || !aligned16(l) || !aligned16(r) || !aligned16(w)) return BAGUA_ERR_UNSUPPORTED;
+    const int nblk = ws ? minmax_partials_blocks(n, Vec<T>::N, 1, ws_bytes) : 0;
+    if (nblk < 1) return BAGUA_ERR_WORKSPACE;
+    hipLaunchKernelGGL(ring_mix_kernel<T>, dim3(nblk), dim3(kBlock), 0, s, static_cast<S*>(t),
+                       static_cast<const S*>(l), static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13,
+                       f53, static_cast<uint2*>(ws));
+    return check_launch();
+}
+
+template <typename T>
+static int apply_impl(const uint8_t* mine, const uint8_t* from_left, const uint8_t* from_right, size_t comp_bytes,
+                      int n, void* t, void* w, void* l, void* r, hipStream_t s) {
+    using S = typename T::storage;
+    constexpr int N = Vec<T>::N;
+    if (!mine || !from_left || !from_right || !t || !w || !l || !r || n < 0) return BAGUA_ERR_INVALID_ARG;
+    if (comp_bytes < (size_t)n + 32) return BAGUA_ERR_INVALID_ARG;
+    if (!aligned16(t) || !aligned16(w) || !aligned16(l) || !aligned16(r)) return BAGUA_ERR_UNSUPPORTED;
+    for (const uint8_t* p : {mine, from_left, from_right})
+        if ((uintptr_t)(p + 32) % N) return BAGUA_ERR_UNSUPPORTED;
+    int64_t blocks = ((int64_t)n / N + kBlock - 1) / kBlock;
+    if (blocks > 2 * kTargetBlocks) blocks = 2 * kTargetBlocks;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(ring_apply_kernel<T>, dim3(blocks), dim3(kBlock), 0, s, mine, from_left, from_right,
+                       static_cast<S*>(t), static_cast<S*>(w), static_cast<S*>(l), static_cast<S*>(r), (int64_t)n);
+    return check_launch();
+}
+
+}  // namespace bagua
+
+using namespace bagua;
+
+extern "C" {
+
+int bagua_ring_mix_minmax(int dtype, void* tensor, const void* left, const void* right, const void* weight,
+                          int num_elem, void* workspace, size_t workspace_bytes, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // :45-60 factors are f64 literals cast to f32, then to T by the 16-bit kernels (K:600)
+    const float f13 = round_to_t(dtype, (float)(1.0 / 3.0)), f53 = round_to_t(dtype, (float)(-5.0 / 3.0));
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return mix_impl<F32>(tensor, left, right, weight, num_elem, workspace, workspace_bytes, f13, f53, s);
+        case BAGUA_DTYPE_F16:
+            return mix_impl<F16>(tensor, left, right, weight, num_elem, workspace, workspace_bytes, f13, f53, s);
+        case BAGUA_DTYPE_BF16:
+            return mix_impl<BF16>(tensor, left, right, weight, num_elem, workspace, workspace_bytes, f13, f53, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+int bagua_ring_apply_minmax(int dtype, const uint8_t* mine, const uint8_t* from_left, const uint8_t* from_right,
+                            size_t compressed_bytes, int num_elem, void* tensor, void* weight, void* left,
+                            void* right, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return apply_impl<F32>(mine, from_left, from_right, compressed_bytes, num_elem, tensor, weight, left,
+                                   right, s);
+        case BAGUA_DTYPE_F16:
+            return apply_impl<F16>(mine, from_left, from_right, compressed_bytes, num_elem, tensor, weight, left,
+                                   right, s);
+        case BAGUA_DTYPE_BF16:
+            return apply_impl<BF16>(mine, from_left, from_right, compressed_bytes, num_elem, tensor, weight, left,
+                                    right, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+}  // extern "C"

@@ -303,6 +303,15 @@ static int blocks_for(int64_t elems, int per_vec, int nact, int sub = kSubtiles,
     return (int)(tiles < 1 ? 1 : tiles);
 }
 
+// workgroups of the min/max pass = partials each chunk's quantise pass folds;
+// shared with producers of the same partials (decentralized.hip)
+int minmax_partials_blocks(int64_t cs, int per_vec, int nact, size_t ws_bytes) {
+    const int nblk = blocks_for(cs, per_vec, nact, kPartialsSub, kPartialsBlocks);
+    const int64_t cap = (int64_t)(ws_bytes / sizeof(uint2)) / (nact > 0 ? nact : 1);
+    if (cap < 1) return 0;
+    return nblk > cap ? (int)cap : nblk;
+}
+
 // stage bit 1: min/max partials pass; bit 2: quantise pass (3 = whole compress).
 // Both stages derive the same partials count from the same arguments.
 template <typename T>
@@ -317,10 +326,8 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
     const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);  // K:537
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     const int nact = target < 0 ? p : 1;
-    int nblk = blocks_for(cs, Vec<T>::N, nact, kPartialsSub, kPartialsBlocks);
-    const int64_t cap = ws ? (int64_t)(ws_bytes / sizeof(uint2)) / nact : 0;
-    if (cap < 1) return BAGUA_ERR_WORKSPACE;
-    if (nblk > cap) nblk = (int)cap;
+    const int nblk = ws ? minmax_partials_blocks(cs, Vec<T>::N, nact, ws_bytes) : 0;
+    if (nblk < 1) return BAGUA_ERR_WORKSPACE;
     uint2* partials = static_cast<uint2*>(ws);
     if (stages & 1)
         hipLaunchKernelGGL(minmax_partials_kernel<T>, dim3(nblk, nact), dim3(kBlock), 0, s,

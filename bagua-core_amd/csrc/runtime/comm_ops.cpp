@@ -294,20 +294,16 @@ int bagua_centralized_full_precision_synchronous(BaguaSingleCommunicatorC* c, co
     return finish(c, rc);
 }
 
-int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t,
-                                                  const bagua_tensor_t* weight, const bagua_tensor_t* left,
-                                                  const bagua_tensor_t* right, int method) {
+static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, const bagua_tensor_t* weight,
+                         const bagua_tensor_t* left, const bagua_tensor_t* right, int method, bool allow_fused) {
     if (!c || !c->t || !t || !weight || !left || !right) return BAGUA_ERR_INVALID_ARG;
     if (c->aborted.load()) return BAGUA_ERR_ABORTED;
     DeviceGuard guard(c->device_id);
     const uint64_t s = (uint64_t)(uintptr_t)c->stream;
+    void* sp = (void*)(uintptr_t)s;
     int rc;
-    // :45-60: t += L/3; t += R/3; t += W*(-5/3)  (f64 literals cast to f32)
-    TRY(bagua_tensor_addmul_inplace(t, left, (float)(1.0 / 3.0), s));
-    TRY(bagua_tensor_addmul_inplace(t, right, (float)(1.0 / 3.0), s));
-    TRY(bagua_tensor_addmul_inplace(t, weight, (float)(-5.0 / 3.0), s));
-    // :61-64 whole-bucket compress (n_chunks = 1)
     if (t->num_elem_allocated > 0x7fffffffULL) return BAGUA_ERR_INVALID_ARG;
+    const int n = (int)t->num_elem_allocated;
     const size_t S = bagua_compressed_size(method, t->dtype, 1, t->num_elem_allocated);
     if (!S) return BAGUA_ERR_UNSUPPORTED;
     PoolBuffer mine, lbuf, rbuf;
@@ -317,7 +313,37 @@ int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* c, c
     const bagua_tensor_t mv = u8_view(mine.ptr(), S, c->device_id);
     const bagua_tensor_t lv = u8_view(lbuf.ptr(), S, c->device_id);
     const bagua_tensor_t rv = u8_view(rbuf.ptr(), S, c->device_id);
-    TRY(bagua_tensor_compress_into(t, method, 1, s, -1, &mv));
+    // fused kernels (csrc/kernels/decentralized.hip) for fully valid, same-shape
+    // MinMax buckets; anything else runs the reference's op sequence
+    bool fused = allow_fused && method == BAGUA_COMPRESSION_MINMAX_UINT8 && t->num_elem == t->num_elem_allocated;
+    for (const bagua_tensor_t* o : {weight, left, right})
+        fused = fused && o->dtype == t->dtype && o->num_elem == t->num_elem;
+    void* tp = (void*)(uintptr_t)t->ptr;
+    void* wp = (void*)(uintptr_t)weight->ptr;
+    void* lp = (void*)(uintptr_t)left->ptr;
+    void* rp = (void*)(uintptr_t)right->ptr;
+    bool mixed = false;
+    if (fused) {
+        // :45-64 t += L/3 + R/3 - 5W/3 (three rounded steps) with the min/max partials, then quantise
+        const size_t wsb = bagua_minmax_u8_workspace_bytes(n, 1);
+        void* ws = (void*)(uintptr_t)stream_workspace(c->device_id, s, wsb);
+        if (!ws) return finish(c, BAGUA_ERR_OOM);
+        rc = bagua_ring_mix_minmax(t->dtype, tp, lp, rp, wp, n, ws, wsb, sp);
+        if (rc == BAGUA_OK) {
+            TRY(bagua_minmax_u8_compress_stage(2, t->dtype, tp, n, n, 1, mine.as<uint8_t>(), S, ws, wsb, -1, sp));
+            mixed = true;
+        } else if (rc != BAGUA_ERR_UNSUPPORTED) {
+            return finish(c, rc);
+        }
+    }
+    if (!mixed) {
+        // :45-60: t += L/3; t += R/3; t += W*(-5/3)  (f64 literals cast to f32)
+        TRY(bagua_tensor_addmul_inplace(t, left, (float)(1.0 / 3.0), s));
+        TRY(bagua_tensor_addmul_inplace(t, right, (float)(1.0 / 3.0), s));
+        TRY(bagua_tensor_addmul_inplace(t, weight, (float)(-5.0 / 3.0), s));
+        // :61-64 whole-bucket compress (n_chunks = 1)
+        TRY(bagua_tensor_compress_into(t, method, 1, s, -1, &mv));
+    }
     // :98-115 ring exchange inside one group
     const int p = (int)c->nranks, r = (int)c->rank;
     const int lpeer = (r + p - 1) % p, rpeer = (r + 1) % p;
@@ -329,6 +355,12 @@ int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* c, c
     const int rc_end = c->t->group_end();
     if (rc || rc_end) return finish(c, rc ? rc : rc_end);
     // :126-151
+    if (fused) {
+        rc = bagua_ring_apply_minmax(t->dtype, mine.as<uint8_t>(), lbuf.as<uint8_t>(), rbuf.as<uint8_t>(), S, n, tp,
+                                     wp, lp, rp, sp);
+        if (rc == BAGUA_OK) return finish(c, BAGUA_OK);
+        if (rc != BAGUA_ERR_UNSUPPORTED) return finish(c, rc);
+    }
     TRY(bagua_tensor_decompress_from(t, method, 1, &lv, s));
     TRY(bagua_tensor_add_inplace(left, t, s));
     TRY(bagua_tensor_decompress_from(t, method, 1, &rv, s));
@@ -337,6 +369,18 @@ int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* c, c
     TRY(bagua_tensor_add_inplace(t, weight, s));
     TRY(bagua_tensor_clone_from(weight, t, s));
     return finish(c, BAGUA_OK);
+}
+
+int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t,
+                                                  const bagua_tensor_t* weight, const bagua_tensor_t* left,
+                                                  const bagua_tensor_t* right, int method) {
+    return decentralized(c, t, weight, left, right, method, true);
+}
+
+int bagua_decentralized_low_precision_synchronous_unfused(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t,
+                                                          const bagua_tensor_t* weight, const bagua_tensor_t* left,
+                                                          const bagua_tensor_t* right, int method) {
+    return decentralized(c, t, weight, left, right, method, false);
 }
 
 }  // extern "C"

@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--pieces", type=int, default=0,
                     help="pipelined all-reduce pieces per chunk (0 = automatic, 1 = unpieced)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-decentralized", action="store_true", help="skip the config-5 side measurement (N > 1)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the cpu_baseline leg")
     return ap.parse_args()
 
@@ -341,6 +342,27 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     t_c = timed(compressed_step, args.steps, args.warmup)
     t_u = timed(lambda: compressed_step(1), max(3, args.steps // 2), max(1, args.warmup // 2))
     t_f = timed(fp32_step, max(3, args.steps // 2), max(1, args.warmup // 2))
+    decentralized = None
+    if not args.no_decentralized:
+        # config 5: bf16 bucket, decentralized ring exchange with the uint8 codec
+        # (decentralized_low_precision_synchronous.rs:42-152), 2^27 elements per rank
+        try:
+            nb = 1 << 27
+            bufs = [(torch.randn(nb, device=dev, generator=g) * 1e-3).to(torch.bfloat16) for _ in range(4)]
+            draws = [BaguaTensorPy(b, k).raw() for b, k in zip(bufs, "twlr")]
+
+            def dec_step():
+                N.check(N.C.bagua_decentralized_low_precision_synchronous(
+                    comm.handle, *[ctypes.byref(r) for r in draws], N.COMPRESSION_MINMAX_UINT8), "decentralized")
+
+            t_d = timed(dec_step, max(3, args.steps // 2), max(1, args.warmup // 2))
+            decentralized = {"config_index": 5, "elements_per_rank": nb, "dtype": "bf16",
+                             "ms_per_step": round(t_d * 1e3, 3),
+                             "gib_s_per_rank": round(2.0 * nb / t_d / GiB, 2),
+                             "gib_s_total": round(world * 2.0 * nb / t_d / GiB, 2)}
+            del bufs, draws
+        except Exception as e:  # noqa: BLE001 - a failed side measurement must not lose the headline line
+            decentralized = {"error": str(e)[:200]}
     value = world * 4.0 * n / t_c / GiB
     per_rank = 4.0 * n / t_c / GiB
     fp32 = 4.0 * n / t_f / GiB
@@ -374,7 +396,9 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     dom = max(range(3), key=lambda i: per[i])
     achieved = alg[dom] / (per[dom] * 1e-3) / 1e9
     roof = {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(names[dom]),
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            # the committed PMC pass is of the 256 MiB codec launch; at this size: unmeasured
+            "traffic": pmc_traffic(names[dom]) if n == (1 << 26) and world == 1 else None,
             "alg_bytes_per_launch": alg[dom], "avg_launch_us": round(per[dom] * 1e3, 2)}
     cfg = {"workload": f"minmax_uint8_compressed_allreduce_{4 * n >> 20}MiB_fp32_per_rank", "bucket_elements": n,
            "n_chunks": world, "collectives": "rccl alltoall + allgather (uint8)", "parallelism": f"dp{world}",
@@ -382,12 +406,18 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     extra = {"per_rank_gib_s": round(per_rank, 2), "fp32_allreduce_gib_s": round(fp32, 2),
              "ratio_vs_fp32": round(per_rank / fp32, 3), "fp32_ms_per_step": round(t_f * 1e3, 3),
              "pieces": args.pieces or "auto", "unpieced_ms_per_step": round(t_u * 1e3, 3),
+             "decentralized_bf16": decentralized,
              "per_kernel_us": {nm: round(t * 1e3, 2) for nm, t in zip(names, per)}}
     del comm
     return value, t_c * 1e3, roof, cfg, extra
 
 
 def main():
+    # Native libraries (RCCL's version banner) write to fd 1; the contract is ONE
+    # JSON line on stdout, so everything else goes to stderr.
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", args.gpus))
     rank = int(os.environ.get("RANK", 0))
@@ -415,7 +445,7 @@ def main():
                         ("in pinned host memory (H2D + D2H timed)" if workload == "host" else "resident in HBM"),
                 "config": cfg, "roofline": roof, "cpu_baseline": cpu}
         line.update(extra)
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     if world > 1:
         import torch.distributed as dist
         if dist.is_initialized():

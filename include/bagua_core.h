@@ -144,6 +144,11 @@ int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* comm
                                                   const bagua_tensor_t* weight,
                                                   const bagua_tensor_t* left_peer_weight,
                                                   const bagua_tensor_t* right_peer_weight, int method);
+/* the reference's unfused op sequence (3 addmul, compress, 3 x decompress + add, clone), for A/B */
+int bagua_decentralized_low_precision_synchronous_unfused(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,
+                                                          const bagua_tensor_t* weight,
+                                                          const bagua_tensor_t* left_peer_weight,
+                                                          const bagua_tensor_t* right_peer_weight, int method);
 
 #ifdef __cplusplus
 }

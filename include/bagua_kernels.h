@@ -138,6 +138,24 @@ int bagua_minmax_u8_requantize_pieces(int dtype, const void* tensor, int chunk_s
                                       size_t output_bytes, int target_chunk, int pieces, const void* workspace,
                                       size_t workspace_bytes, bagua_stream_t stream);
 
+/* Decentralized ring op (decentralized_low_precision_synchronous.rs:45-64,126-151)
+ * as two fused passes around the MinMax quantise pass, bit-identical to the
+ * reference's elementwise sequence (every intermediate rounded to T where the
+ * reference stores it):
+ *   bagua_ring_mix_minmax: tensor = ((tensor + L/3) + R/3) + W*(-5/3), each an
+ *     addmul as bagua_addmul_inplace computes it, and the min/max partials of the
+ *     result into `workspace` exactly as stage 1 of bagua_minmax_u8_compress_stage
+ *     (n_chunks = 1, same workspace_bytes) would; follow with stage 2.
+ *   bagua_ring_apply_minmax: L += dq(from_left); R += dq(from_right);
+ *     tensor = dq(mine) + W; W = tensor (n_chunks = 1 MinMax buffers).
+ * Both return BAGUA_ERR_UNSUPPORTED for tensors not 16-B aligned (callers run the
+ * elementwise sequence). */
+int bagua_ring_mix_minmax(int dtype, void* tensor, const void* left, const void* right, const void* weight,
+                          int num_elem, void* workspace, size_t workspace_bytes, bagua_stream_t stream);
+int bagua_ring_apply_minmax(int dtype, const uint8_t* mine, const uint8_t* from_left, const uint8_t* from_right,
+                            size_t compressed_bytes, int num_elem, void* tensor, void* weight, void* left,
+                            void* right, bagua_stream_t stream);
+
 /* K:196-266 elementwise kernels, dtype-generic (f32, f16, bf16) */
 int bagua_add_inplace(int dtype, void* x, const void* y, int n, bagua_stream_t stream);
 int bagua_addmul_inplace(int dtype, void* x, const void* y, int n, float factor, bagua_stream_t stream);

@@ -86,14 +86,17 @@ def minmax(x: np.ndarray, dtype: int) -> tuple[float, float]:
 
 
 def compress_minmax_u8(x: np.ndarray, dtype: int, n_chunks: int, target_chunk: int = -1,
-                       out: np.ndarray | None = None) -> np.ndarray:
-    """BaguaTensor.compress("MinMaxUInt8", n_chunks, target_chunk) on a host array."""
+                       out: np.ndarray | None = None, num_elem: int | None = None) -> np.ndarray:
+    """BaguaTensor.compress("MinMaxUInt8", n_chunks, target_chunk) on a host array.
+    `num_elem` (default x.size) is the tensor's num_elements(): elements past it
+    are not part of the min/max and quantise to 0 (DT:339, K:455-479)."""
     assert x.size % n_chunks == 0, "compression tensor size % n_chunks must be 0"
     cs = x.size // n_chunks
     size = minmax_compressed_size(n_chunks, cs, dtype)
     if out is None:
         out = np.zeros(size, dtype=np.uint8)
-    rc = lib().orc_compress_minmax_u8(_ptr(x), dtype, x.size, cs, n_chunks, _ptr(out), size, target_chunk)
+    n = x.size if num_elem is None else int(num_elem)
+    rc = lib().orc_compress_minmax_u8(_ptr(x), dtype, n, cs, n_chunks, _ptr(out), size, target_chunk)
     assert rc == 0, rc
     return out
 

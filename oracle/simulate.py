@@ -17,9 +17,15 @@ import numpy as np
 
 
 def centralized_low_precision(backend, inputs: list[np.ndarray], dtype: int, average: bool = True,
-                              method: str = "MinMaxUInt8") -> list[np.ndarray]:
+                              method: str = "MinMaxUInt8", num_elem: int | None = None) -> list[np.ndarray]:
+    """`num_elem` < allocated size: the tensors' num_elements() (oracle_c MinMax only)."""
     p = len(inputs)
     comp = backend.compress_minmax_u8 if method == "MinMaxUInt8" else backend.compress_onebit
+    if num_elem is not None:
+        base_comp = comp
+
+        def comp(t, dtype, n_chunks, target, out=None):
+            return base_comp(t, dtype, n_chunks, target, out=out, num_elem=num_elem)
     decomp = backend.decompress_minmax_u8 if method == "MinMaxUInt8" else backend.decompress_onebit
     ts = [x.copy() for x in inputs]
     send = [comp(t, dtype, p, -1) for t in ts]

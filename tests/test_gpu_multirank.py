@@ -113,6 +113,32 @@ def test_centralized_pipelined_multirank(bc, oracle_c, p, dtype, cs, pieces):
         assert np.array_equal(host(ts[r], dtype).view(np.uint8), want[r].view(np.uint8)), f"rank {r}"
 
 
+@pytest.mark.parametrize("p,dtype,short", [(2, F32, 37), (4, BF16, 1000), (3, F32, 4096 + 5)])
+def test_centralized_partially_valid_tensor(bc, oracle_c, p, dtype, short):
+    """num_elem < num_elem_allocated: the reference compresses num_elements()
+    (DT:339); the op must run the unfused sequence and match it bit-for-bit."""
+    from bagua_core.communicator import loopback_communicators
+    cs = 12288
+    n = p * cs
+    rng = np.random.default_rng(7 * p + short)
+    xs = [NP.from_f32((rng.standard_normal(n) * 1e-3 + 0.5 * r).astype(np.float32), dtype) for r in range(p)]
+    want = simulate.centralized_low_precision(oracle_c, xs, dtype, True, num_elem=n - short)
+    comms = loopback_communicators(p, 0)
+    ts = [dev(x, dtype) for x in xs]
+    torch.cuda.synchronize()
+    N = bc._native
+
+    def rank(r):
+        raw = bc.BaguaTensorPy(ts[r], f"g{r}").raw()
+        raw.num_elem = n - short
+        N.check(N.C.bagua_centralized_low_precision_synchronous(comms[r].handle, ctypes.byref(raw), 1,
+                                                                N.COMPRESSION_MINMAX_UINT8), f"rank {r}")
+
+    run_ranks(rank, p)
+    for r in range(p):
+        assert np.array_equal(host(ts[r], dtype).view(np.uint8), want[r].view(np.uint8)), f"rank {r}"
+
+
 @pytest.mark.parametrize("p", [2, 4])
 def test_centralized_onebit_multirank(bc, oracle_c, p):
     from bagua_core.communicator import loopback_communicators
@@ -135,23 +161,33 @@ def test_centralized_onebit_multirank(bc, oracle_c, p):
         assert np.array_equal(host(ts[r], F32).view(np.uint32), want[r].view(np.uint32)), f"rank {r}"
 
 
-@pytest.mark.parametrize("p,dtype", [(2, F32), (3, F32), (4, BF16), (8, F32)])
-def test_decentralized_low_precision_multirank(bc, oracle_c, p, dtype):
+@pytest.mark.parametrize("p,dtype,n,unfused,offset", [(2, F32, 30011, False, 0), (3, F32, 30011, False, 0),
+                                                     (4, BF16, 30011, False, 0), (8, F32, 30011, False, 0),
+                                                     (2, F16, 65536 + 7, False, 0), (2, BF16, (1 << 20) + 3, False, 0),
+                                                     (4, BF16, 30011, True, 0), (2, F32, 4099, False, 1)])
+def test_decentralized_low_precision_multirank(bc, oracle_c, p, dtype, n, unfused, offset):
+    """Fused ring kernels (decentralized.hip) and the reference sequence (`unfused`, or a
+    misaligned tensor: offset elements) against the oracle's op simulation, every tensor."""
     from bagua_core.communicator import loopback_communicators
-    n = 30011
-    rng = np.random.default_rng(50 + p)
+    rng = np.random.default_rng(50 + p + n)
     arrs = {k: [NP.from_f32((rng.standard_normal(n) * 1e-3).astype(np.float32), dtype) for _ in range(p)]
             for k in "twlr"}
     want = simulate.decentralized_low_precision(oracle_c, arrs["t"], arrs["w"], arrs["l"], arrs["r"], dtype)
     comms = loopback_communicators(p, 0)
-    dts = {k: [dev(a, dtype) for a in arrs[k]] for k in "twlr"}
+
+    def place(a):
+        full = dev(np.concatenate([np.zeros(offset, a.dtype), a]), dtype)
+        return full[offset:]
+
+    dts = {k: [place(a) for a in arrs[k]] for k in "twlr"}
     torch.cuda.synchronize()
     N = bc._native
+    fn = (N.C.bagua_decentralized_low_precision_synchronous_unfused if unfused
+          else N.C.bagua_decentralized_low_precision_synchronous)
 
     def rank(r):
         raws = [bc.BaguaTensorPy(dts[k][r], k).raw() for k in "twlr"]
-        N.check(N.C.bagua_decentralized_low_precision_synchronous(comms[r].handle, *[ctypes.byref(x) for x in raws],
-                                                                  N.COMPRESSION_MINMAX_UINT8), f"rank {r}")
+        N.check(fn(comms[r].handle, *[ctypes.byref(x) for x in raws], N.COMPRESSION_MINMAX_UINT8), f"rank {r}")
 
     run_ranks(rank, p)
     for k, wk in zip("twlr", want):
