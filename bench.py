@@ -285,7 +285,18 @@ def cpu_baseline(args, sample_elems: int = 1 << 24):
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds or reps >= 100000:
             break
+    # config 1: 4 MiB fp32, the whole centralized op sequence (compress -> alltoall ->
+    # decompress -> reduce -> compress -> allgather -> decompress) at p = 1 on the CPU path
+    from oracle import simulate
+    x1 = [(rng.standard_normal(1 << 20) * 1e-3).astype(np.float32)]
+    simulate.centralized_low_precision(oracle_c, x1, 0, True)
+    r1, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < 1.0:
+        simulate.centralized_low_precision(oracle_c, x1, 0, True)
+        r1 += 1
+    cfg1 = round(4.0 * (1 << 20) * r1 / (time.perf_counter() - t1) / GiB, 3)
     return {"value": round(4.0 * sample_elems * reps / el / GiB, 3), "unit": "GiB/s", "cores": lib_threads,
+            "config1_loopback_op_gib_s": cfg1,
             "kind": "port",
             "sample": f"{4 * sample_elems >> 20} MiB fp32 N(0,1e-3^2) bucket, MinMax-UInt8 encode+decode x{reps} "
                       f"({el:.1f} s wall, {lib_threads} OpenMP threads, oracle/bagua_oracle.c)"}
