@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=["auto", "codec", "allreduce", "onebit", "host"], default="auto")
     ap.add_argument("--elements", type=int, default=0, help="override bucket elements")
+    ap.add_argument("--dtype", choices=["f32", "f16", "bf16"], default="f32",
+                    help="codec workloads: gradient dtype (the headline is f32; bf16/f16 buckets keep 256 MiB)")
     ap.add_argument("--pieces", type=int, default=0,
                     help="pipelined all-reduce pieces per chunk (0 = automatic, 1 = unpieced)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -74,12 +76,14 @@ def pmc_traffic(kernel: str):
 def bench_codec(args, onebit: bool = False):
     from bagua_core import _native as N
     K = N.K
-    n = args.elements or (1 << 26)
+    dcode, tdt, esz = {"f32": (0, torch.float32, 4), "f16": (1, torch.float16, 2),
+                       "bf16": (2, torch.bfloat16, 2)}[args.dtype]
+    n = args.elements or ((1 << 28) // esz)  # a 256 MiB bucket
     p = 1
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     g = torch.Generator(device=dev).manual_seed(0x5EED)
-    x = torch.randn(n, device=dev, generator=g) * 1e-3
+    x = (torch.randn(n, device=dev, generator=g) * 1e-3).to(tdt)
     y = torch.empty_like(x)
     stream = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
@@ -87,7 +91,7 @@ def bench_codec(args, onebit: bool = False):
         S = K.bagua_onebit_compressed_bytes(n, p)
         ws_bytes = K.bagua_onebit_workspace_bytes(n, p)
     else:
-        S = K.bagua_minmax_u8_compressed_bytes(0, n, p)
+        S = K.bagua_minmax_u8_compressed_bytes(dcode, n, p)
         ws_bytes = K.bagua_minmax_u8_workspace_bytes(n, p)
     comp = torch.empty(S, dtype=torch.uint8, device=dev)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
@@ -97,19 +101,19 @@ def bench_codec(args, onebit: bool = False):
         names = ["onebit_encode+finalize", "onebit_decode"]
 
         def launches():
-            return [lambda: K.bagua_onebit_compress(0, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
-                    lambda: K.bagua_onebit_decompress(0, cp, S, n, p, yp, sp)]
-        alg = [4 * n + n // 8 + 32, n // 8 + 32 + 4 * n]
+            return [lambda: K.bagua_onebit_compress(dcode, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
+                    lambda: K.bagua_onebit_decompress(dcode, cp, S, n, p, yp, sp)]
+        alg = [esz * n + n // 8 + 32, n // 8 + 32 + esz * n]
     else:
         names = ["minmax_partials_kernel", "minmax_quantize_kernel", "minmax_dequantize_kernel"]
 
         def launches():
-            return [lambda: K.bagua_minmax_u8_compress_stage(1, 0, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
-                    lambda: K.bagua_minmax_u8_compress_stage(2, 0, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
-                    lambda: K.bagua_minmax_u8_decompress(0, cp, S, n, p, yp, sp)]
+            return [lambda: K.bagua_minmax_u8_compress_stage(1, dcode, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
+                    lambda: K.bagua_minmax_u8_compress_stage(2, dcode, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
+                    lambda: K.bagua_minmax_u8_decompress(dcode, cp, S, n, p, yp, sp)]
         # algorithmic bytes per launch: partials read 4N; quantise read 4N + write N + header;
         # dequantise read N + header, write 4N.  Sum = 14N + 64p.
-        alg = [4 * n, 4 * n + n + 32, n + 32 + 4 * n]
+        alg = [esz * n, esz * n + n + 32, n + 32 + esz * n]
     calls = launches()
 
     def step():
@@ -150,12 +154,12 @@ def bench_codec(args, onebit: bool = False):
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     ms = wall * 1e3 / args.steps
-    value = 4.0 * n / (ms * 1e-3) / GiB
+    value = esz * n / (ms * 1e-3) / GiB  # gradient bytes processed (4N fp32, 2N bf16)
     dom_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     per[dom] = dom_ms
     achieved = alg[dom] / (per[dom] * 1e-3) / 1e9
     step_alg = sum(alg)
-    traffic = pmc_traffic(names[dom])
+    traffic = pmc_traffic(names[dom]) if (args.dtype == "f32" and n == (1 << 26) and not onebit) else None
     roof = {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "alg_bytes_per_launch": alg[dom], "avg_launch_us": round(per[dom] * 1e3, 2)}
@@ -167,11 +171,11 @@ def bench_codec(args, onebit: bool = False):
                           "achieved_gbs": round(step_alg / (ms * 1e-3) / 1e9, 1),
                           "frac": round(step_alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "per_kernel_note": "dominant kernel: timed-region events; others: warmup events between launches",
-        "encode_gib_s": round(4.0 * n / (sum(per[:-1]) * 1e-3) / GiB, 1),
-        "decode_gib_s": round(4.0 * n / (per[-1] * 1e-3) / GiB, 1),
+        "encode_gib_s": round(esz * n / (sum(per[:-1]) * 1e-3) / GiB, 1),
+        "decode_gib_s": round(esz * n / (per[-1] * 1e-3) / GiB, 1),
     }
     cfg = {"workload": ("onebit_sign_scale" if onebit else "minmax_uint8") +
-           f"_encode_decode_{4 * n >> 20}MiB_fp32_bucket", "bucket_elements": n, "n_chunks": p,
+           f"_encode_decode_{esz * n >> 20}MiB_{args.dtype}_bucket", "bucket_elements": n, "n_chunks": p,
            "compressed_bytes": S, "config_index": 3 if onebit else 2}
     return value, ms, roof, cfg, extra, x
 
@@ -441,7 +445,7 @@ def main():
         value, ms, roof, cfg, extra, _ = bench_codec(args, onebit=(workload == "onebit"))
         if rank == 0 and world == 1 and not args.no_cpu_baseline and workload == "codec":
             cpu = cpu_baseline(args)
-        dtype = "f32 -> u8" if workload == "codec" else "f32 -> 1bit"
+        dtype = f"{args.dtype} -> u8" if workload == "codec" else f"{args.dtype} -> 1bit"
     elif workload == "host":
         value, ms, roof, cfg, extra = bench_host(args)
         dtype = "f32 -> u8"

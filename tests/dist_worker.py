@@ -43,6 +43,68 @@ def centralized_rank(rank: int, world: int, port: int, inputs_path: str, out_dir
         dist.destroy_process_group()
 
 
+def _piece_range(cs: int, pieces: int, q: int) -> tuple[int, int]:
+    """bagua_minmax_u8_piece_range from the built kernel library (host-only function)."""
+    import ctypes
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = ctypes.CDLL(os.path.join(root, "bagua-core_amd", "lib", "libbagua_kernels.so"))
+    b, e = ctypes.c_int(), ctypes.c_int()
+    assert lib.bagua_minmax_u8_piece_range(cs, pieces, q, ctypes.byref(b), ctypes.byref(e)) == 0
+    return b.value, e.value
+
+
+def _piece_bytes(cs: int, co: int, pieces: int, q: int) -> tuple[int, int]:
+    # comm_ops.cpp piece_bytes: header with piece 0, slack with the last non-empty piece
+    b, e = _piece_range(cs, pieces, q)
+    if q > 0 and b == e:
+        return 0, 0
+    return (0 if q == 0 else 32 + b), (co if e == cs else 32 + e)
+
+
+def centralized_pieced_rank(rank: int, world: int, port: int, inputs_path: str, out_dir: str, dtype: int,
+                            pieces: int) -> None:
+    """The pipelined op's exchange protocol (comm_ops.cpp centralized_pipelined): every
+    alltoall / allgather moves one byte range of every segment per piece."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        with np.load(inputs_path, allow_pickle=False) as z:
+            t = z[f"x{rank}"].copy()
+        p = world
+        cs = t.size // p
+        send = C.compress_minmax_u8(t, dtype, p, -1)
+        S = send.size
+        co = S // p
+        recv = np.full(S, 0xAB, np.uint8)  # poison: every byte must arrive through a piece
+        for q in range(pieces):
+            lo, hi = _piece_bytes(cs, co, pieces, q)
+            if hi <= lo:
+                continue
+            part = torch.from_numpy(np.concatenate([send[j * co + lo:j * co + hi] for j in range(p)]))
+            got = torch.empty_like(part)
+            dist.all_to_all_single(got, part)
+            g = got.numpy()
+            for j in range(p):
+                recv[j * co + lo:j * co + hi] = g[j * (hi - lo):(j + 1) * (hi - lo)]
+        C.decompress_minmax_u8(recv, p, t, dtype)
+        C.reduce_chunks(t, dtype, p, rank, True)
+        C.compress_minmax_u8(t, dtype, p, rank, out=send)
+        for q in range(pieces):
+            lo, hi = _piece_bytes(cs, co, pieces, q)
+            if hi <= lo:
+                continue
+            got = torch.empty(p * (hi - lo), dtype=torch.uint8)
+            dist.all_gather_into_tensor(got, torch.from_numpy(send[rank * co + lo:rank * co + hi].copy()))
+            g = got.numpy()
+            for j in range(p):
+                send[j * co + lo:j * co + hi] = g[j * (hi - lo):(j + 1) * (hi - lo)]
+        C.decompress_minmax_u8(send, p, t, dtype)
+        np.save(os.path.join(out_dir, f"out{rank}.npy"), t.view(np.uint8))
+    finally:
+        dist.destroy_process_group()
+
+
 def decentralized_rank(rank: int, world: int, port: int, inputs_path: str, out_dir: str, dtype: int) -> None:
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

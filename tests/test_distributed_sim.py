@@ -40,6 +40,24 @@ def test_centralized_gloo(tmp_path, world, dtype, cs):
         assert np.array_equal(outs[r], outs[0])
 
 
+@pytest.mark.parametrize("world,dtype,cs,pieces", [(2, 0, 5000, 3), (4, 0, 1031 * 8, 4), (2, 2, 1536, 4)])
+def test_centralized_pieced_gloo(tmp_path, world, dtype, cs, pieces):
+    """The pipelined op's per-piece byte ranges (real bagua_minmax_u8_piece_range) moved
+    between gloo processes reproduce the unpieced op bit-for-bit."""
+    oracle_c.build()
+    rng = np.random.default_rng(world * 11 + dtype + pieces)
+    xs = [NP.from_f32((rng.standard_normal(world * cs) * 1e-3).astype(np.float32), dtype) for _ in range(world)]
+    if oracle_c.minmax_compressed_size(world, cs, dtype) % world:
+        pytest.skip("reference alltoall requires S % nranks == 0")
+    inputs = tmp_path / "in.npz"
+    np.savez(inputs, **{f"x{r}": x for r, x in enumerate(xs)})
+    mp.spawn(dist_worker.centralized_pieced_rank, args=(world, _free_port(), str(inputs), str(tmp_path), dtype,
+                                                         pieces), nprocs=world, join=True)
+    want = simulate.centralized_low_precision(oracle_c, xs, dtype, True)
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"out{r}.npy"), want[r].view(np.uint8)), f"rank {r}"
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_decentralized_ring_gloo(tmp_path, world):
     oracle_c.build()
