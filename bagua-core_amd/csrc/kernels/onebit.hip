@@ -12,6 +12,8 @@
 // 64-lane xor butterfly per tile, then the same 1024-tree over the tile
 // partials), so the encoder is single-pass over the input and its result is
 // independent of grid size and bit-reproducible against the oracle.
+#include <type_traits>
+
 #include "codec_common.hpp"
 #include "launch_util.hpp"
 
@@ -44,6 +46,18 @@ __device__ __forceinline__ void load4(const typename T::storage* p, int64_t j, i
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e) f[e] = (j + e < n) ? T::load(p, j + e) : 0.0f;
+}
+
+// 4 elements from one 16-B (f32) / 8-B (16-bit) load
+template <typename T>
+__device__ __forceinline__ void unpack4(const uint4& v, float (&f)[4]) {
+    f[0] = __uint_as_float(v.x); f[1] = __uint_as_float(v.y);
+    f[2] = __uint_as_float(v.z); f[3] = __uint_as_float(v.w);
+}
+template <typename T>
+__device__ __forceinline__ void unpack4(const uint2& v, float (&f)[4]) {
+    f[0] = T::to_f((uint16_t)(v.x & 0xffff)); f[1] = T::to_f((uint16_t)(v.x >> 16));
+    f[2] = T::to_f((uint16_t)(v.y & 0xffff)); f[3] = T::to_f((uint16_t)(v.y >> 16));
 }
 
 template <typename T>
@@ -97,27 +111,56 @@ __global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
     const int lane = lane_id();
     const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
-    for (int64_t t = wave; t < tiles_per_chunk; t += nwaves) {
-        float a[4][4];
+    // a lane reads 4 consecutive elements per sub-tile: 16 B for f32 but only 8 B
+    // for 16-bit types, so those take two tiles per iteration (8 loads in flight)
+    constexpr int TPI = sizeof(S) == 4 ? 1 : 2;
+    for (int64_t t0 = wave * TPI; t0 < tiles_per_chunk; t0 += nwaves * TPI) {
+        float a[TPI][4][4];
+        if (vec && (t0 + TPI) * kObTile <= n) {
+            // full tiles: every load issued unconditionally before any is used (a
+            // guarded load gets its own s_waitcnt vmcnt(0) and the wave serialises)
+            using L = std::conditional_t<sizeof(S) == 4, uint4, uint2>;  // 4 elements: 16 B (f32) / 8 B
+            L raw[TPI][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) load4<T>(src, t * kObTile + k * 256 + lane * 4, n, vec, a[k]);
-        uint32_t word = 0;  // lane l < 32 stores dword l of the 128-byte tile
+            for (int u = 0; u < TPI; ++u)
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+                for (int k = 0; k < 4; ++k) {
+                    const S* p = src + (t0 + u) * kObTile + k * 256 + lane * 4;
+                    if constexpr (sizeof(S) == 4) raw[u][k] = nt_load16(p);
+                    else raw[u][k] = nt_load8(p);
+                }
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint64_t m = __ballot(a[k][e] < 0.0f);
-                const int w = k * 4 + e;
-                if ((lane >> 1) == w) word = (lane & 1) ? (uint32_t)(m >> 32) : (uint32_t)m;
-            }
-        if (lane < 32) reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane] = word;
-        float ab[4][4];
+            for (int u = 0; u < TPI; ++u)
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+                for (int k = 0; k < 4; ++k) unpack4<T>(raw[u][k], a[u][k]);
+        } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) ab[k][e] = __builtin_fabsf(a[k][e]);
-        const float s = wave_tree_sum(lane_tree(ab));
-        if (lane == 0) part[t] = s;
+            for (int u = 0; u < TPI; ++u)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) load4<T>(src, (t0 + u) * kObTile + k * 256 + lane * 4, n, vec, a[u][k]);
+        }
+#pragma unroll
+        for (int u = 0; u < TPI; ++u) {
+            const int64_t t = t0 + u;
+            if (t >= tiles_per_chunk) break;
+            uint32_t word = 0;  // lane l < 32 stores dword l of the 128-byte tile
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint64_t m = __ballot(a[u][k][e] < 0.0f);
+                    const int w = k * 4 + e;
+                    if ((lane >> 1) == w) word = (lane & 1) ? (uint32_t)(m >> 32) : (uint32_t)m;
+                }
+            if (lane < 32) reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane] = word;
+            float ab[4][4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) ab[k][e] = __builtin_fabsf(a[u][k][e]);
+            const float s = wave_tree_sum(lane_tree(ab));
+            if (lane == 0) part[t] = s;
+        }
     }
 }
 
