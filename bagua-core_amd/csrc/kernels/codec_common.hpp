@@ -254,6 +254,35 @@ __device__ __forceinline__ void load_bytes(const uint8_t* p, uint32_t (&b)[Vec<T
     }
 }
 
+// --------------------------------------------------- dequantisation tables --
+// A segment's payload byte has 256 possible values, so a workgroup evaluates
+// dequant() once per value into LDS and each element becomes one table read
+// instead of a correctly rounded f32 division (~10 VALU ops).  Entries are
+// computed by the very same expression, so results are bit-identical.
+// Stored form: the T bits the reference's decompress writes (f32 bits, or the
+// 16-bit pattern zero-extended).
+template <typename T>
+__device__ __forceinline__ uint32_t stored_bits(float f) {
+    if constexpr (sizeof(typename T::storage) == 4) return __float_as_uint(f);
+    else return (uint32_t)T::from_f(f);
+}
+template <typename T>
+__device__ __forceinline__ float from_stored_bits(uint32_t u) {
+    if constexpr (sizeof(typename T::storage) == 4) return __uint_as_float(u);
+    else return T::to_f((typename T::storage)u);
+}
+template <typename T>
+__device__ __forceinline__ typename T::storage storage_from_bits(uint32_t u) {
+    if constexpr (sizeof(typename T::storage) == 4) return __uint_as_float(u);
+    else return (typename T::storage)u;
+}
+// one 16-B vector of T from N table entries (bits as stored)
+template <typename T>
+__device__ __forceinline__ uint4 pack_stored(const uint32_t (&u)[Vec<T>::N]) {
+    if constexpr (Vec<T>::N == 4) return make_uint4(u[0], u[1], u[2], u[3]);
+    else return make_uint4(u[0] | (u[1] << 16), u[2] | (u[3] << 16), u[4] | (u[5] << 16), u[6] | (u[7] << 16));
+}
+
 template <typename T>
 __device__ __forceinline__ QParams read_header(const uint8_t* seg) {
     using S = typename T::storage;

@@ -98,6 +98,13 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
                                                             typename T::storage* __restrict__ r, int64_t n) {
     constexpr int N = Vec<T>::N;
     const QParams qm = read_header<T>(mine), ql = read_header<T>(from_left), qr = read_header<T>(from_right);
+    // per-byte dequantised values of the three buffers (codec_common.hpp "dequantisation tables")
+    static_assert(kBlock == 256, "one table entry per thread");
+    __shared__ float tm[256], tl[256], tr[256];
+    tm[threadIdx.x] = as_stored<T>(dequant(threadIdx.x, qm));
+    tl[threadIdx.x] = as_stored<T>(dequant(threadIdx.x, ql));
+    tr[threadIdx.x] = as_stored<T>(dequant(threadIdx.x, qr));
+    __syncthreads();
     const uint8_t* pm = mine + 32;
     const uint8_t* pl = from_left + 32;
     const uint8_t* pr = from_right + 32;
@@ -117,9 +124,9 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
         unpack16<T>(rw, fw);
 #pragma unroll
         for (int i = 0; i < N; ++i) {
-            fl[i] = fl[i] + as_stored<T>(dequant(bl[i], ql));   // L += dq(from_left)
-            fr[i] = fr[i] + as_stored<T>(dequant(br[i], qr));   // R += dq(from_right)
-            ft[i] = as_stored<T>(dequant(bm[i], qm)) + fw[i];   // t = dq(mine) + W
+            fl[i] = fl[i] + tl[bl[i]];   // L += dq(from_left)
+            fr[i] = fr[i] + tr[br[i]];   // R += dq(from_right)
+            ft[i] = tm[bm[i]] + fw[i];   // t = dq(mine) + W
         }
         const uint4 ot = pack16<T>(ft);
         nt_store16(pack16<T>(fl), reinterpret_cast<uint4*>(l) + v);
@@ -129,9 +136,9 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
     }
     if (blockIdx.x == 0 && threadIdx.x < n - nvec * N) {
         const int64_t j = nvec * N + threadIdx.x;
-        l[j] = T::from_f(T::to_f(l[j]) + as_stored<T>(dequant(pl[j], ql)));
-        r[j] = T::from_f(T::to_f(r[j]) + as_stored<T>(dequant(pr[j], qr)));
-        const typename T::storage o = T::from_f(as_stored<T>(dequant(pm[j], qm)) + T::to_f(w[j]));
+        l[j] = T::from_f(T::to_f(l[j]) + tl[pl[j]]);
+        r[j] = T::from_f(T::to_f(r[j]) + tr[pr[j]]);
+        const typename T::storage o = T::from_f(tm[pm[j]] + T::to_f(w[j]));
         t[j] = o;
         w[j] = o;
     }

@@ -240,11 +240,15 @@ __global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
     const uint8_t* payload = seg + 32 + e0;
     S* dst = out + (int64_t)c * cs + e0;
     const int64_t len = e1 - e0;
+    static_assert(kBlock == 256, "one table entry per thread");
+    __shared__ uint32_t lut[256];  // stored T bits of every byte value (codec_common.hpp)
+    lut[threadIdx.x] = stored_bits<T>(dequant(threadIdx.x, q));
+    __syncthreads();
 
     const int a = common_alignment<T>((uintptr_t)dst, (uintptr_t)payload);
     if (a < 0) {
         for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < len; j += (int64_t)gridDim.x * kBlock)
-            dst[j] = T::from_f(dequant(payload[j], q));
+            dst[j] = storage_from_bits<T>(lut[payload[j]]);
         return;
     }
     const int64_t j0 = a < len ? a : len;
@@ -264,10 +268,9 @@ __global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
             for (int k = 0; k < kSubtiles; ++k) {
                 uint32_t b[N];
                 split_bytes<T>(raw[k], b);
-                float f[N];
 #pragma unroll
-                for (int i = 0; i < N; ++i) f[i] = dequant(b[i], q);
-                nt_store16(pack16<T>(f), &vdst[base + k * kBlock + threadIdx.x]);
+                for (int i = 0; i < N; ++i) b[i] = lut[b[i]];
+                nt_store16(pack_stored<T>(b), &vdst[base + k * kBlock + threadIdx.x]);
             }
             continue;
         }
@@ -276,16 +279,15 @@ __global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
             if (v >= nvec) continue;
             uint32_t b[N];
             split_bytes<T>(load_word<T>(vsrc + v * N), b);
-            float f[N];
 #pragma unroll
-            for (int i = 0; i < N; ++i) f[i] = dequant(b[i], q);
-            nt_store16(pack16<T>(f), &vdst[v]);
+            for (int i = 0; i < N; ++i) b[i] = lut[b[i]];
+            nt_store16(pack_stored<T>(b), &vdst[v]);
         }
     }
     if (blockIdx.x == 0) {
-        for (int64_t j = threadIdx.x; j < j0; j += kBlock) dst[j] = T::from_f(dequant(payload[j], q));
+        for (int64_t j = threadIdx.x; j < j0; j += kBlock) dst[j] = storage_from_bits<T>(lut[payload[j]]);
         for (int64_t j = j0 + nvec * N + threadIdx.x; j < len; j += kBlock)
-            dst[j] = T::from_f(dequant(payload[j], q));
+            dst[j] = storage_from_bits<T>(lut[payload[j]]);
     }
 }
 

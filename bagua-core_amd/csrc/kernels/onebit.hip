@@ -113,7 +113,7 @@ __global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     // a lane reads 4 consecutive elements per sub-tile: 16 B for f32 but only 8 B
     // for 16-bit types, so those take two tiles per iteration (8 loads in flight)
-    constexpr int TPI = sizeof(S) == 4 ? 1 : 2;
+    constexpr int TPI = 2;
     for (int64_t t0 = wave * TPI; t0 < tiles_per_chunk; t0 += nwaves * TPI) {
         float a[TPI][4][4];
         if (vec && (t0 + TPI) * kObTile <= n) {

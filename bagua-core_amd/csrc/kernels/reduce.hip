@@ -135,13 +135,39 @@ static int reduce_impl(void* x, int cs, int p, int target, int average, hipStrea
 }
 
 // ---------------------------------------------- fused dequantise + reduce --
-template <typename T, int BY, bool AVG, bool PARTIALS>
+// EPL payload bytes of one segment as one load (4, 8 or 16 B)
+template <int EPL>
+struct ByteWord;
+template <> struct ByteWord<4> { using type = uint32_t; };
+template <> struct ByteWord<8> { using type = uint2; };
+template <> struct ByteWord<16> { using type = uint4; };
+
+template <int EPL>
+__device__ __forceinline__ typename ByteWord<EPL>::type load_payload(const uint8_t* p) {
+    if constexpr (EPL == 4) return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
+    else if constexpr (EPL == 8) return nt_load8(p);
+    else return nt_load16(p);
+}
+template <int EPL>
+__device__ __forceinline__ uint32_t payload_byte(const typename ByteWord<EPL>::type& w, int i) {
+    uint32_t d;
+    if constexpr (EPL == 4) d = w;
+    else if constexpr (EPL == 8) d = (i < 4) ? w.x : w.y;
+    else d = (i < 4) ? w.x : (i < 8) ? w.y : (i < 12) ? w.z : w.w;
+    return (d >> (8 * (i & 3))) & 0xffu;
+}
+
+// Each lane reduces EPL consecutive elements per step: one EPL-byte load per
+// segment (16 B where the segments allow it, so a lane keeps BY x 16 B in
+// flight), summed in the reference's tree order (block_y_reduce, K:171-194).
+template <typename T, int BY, bool AVG, bool PARTIALS, int EPL>
 __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
     const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t e0, int64_t cs, int p,
     typename T::storage* __restrict__ out, uint2* __restrict__ partials) {
     // reduces elements [e0, e0 + cs) of the chunk (`out` points at element e0)
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
+    static_assert(EPL % N == 0, "whole output vectors per lane");
     __shared__ QParams qp[kMaxFusedChunks];
     for (int c = threadIdx.x; c < p; c += kBlock) {
         const uint8_t* seg = in + (int64_t)c * chunk_offset;
@@ -151,73 +177,76 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
         qp[c] = make_qparams(T::to_f(hmn), T::to_f(hmx));
     }
     __syncthreads();
+    // dequantised value of every byte of every segment, as the reference stores
+    // it in T before reducing (codec_common.hpp "dequantisation tables")
+    __shared__ float lut[kMaxFusedChunks][256];
+    for (int i = threadIdx.x; i < p * 256; i += kBlock) lut[i >> 8][i & 255] = as_stored<T>(dequant(i & 255, qp[i >> 8]));
+    __syncthreads();
     const float pf = (float)p;
     uint32_t lo = min_space(T::init_max()), hi = max_space(-T::init_max());
-    // fast path needs every segment's payload N-byte aligned and out 16-B aligned (checked on host)
-    const int64_t nvec = cs / N;
-    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * kBlock) {
-        float s[N][BY];
+    // fast path: every segment's payload EPL-byte aligned and out 16-B aligned (checked on host)
+    const int64_t ngrp = cs / EPL;
+    const uint8_t* base = in + 32 + e0;
+    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < ngrp; g += (int64_t)gridDim.x * kBlock) {
+        float s[EPL][BY];
 #pragma unroll
-        for (int i = 0; i < N; ++i)
+        for (int i = 0; i < EPL; ++i)
 #pragma unroll
             for (int y = 0; y < BY; ++y) s[i][y] = 0.0f;
         for (int r = 0; r * BY < p; ++r) {
-            uint32_t b[BY][N];
+            typename ByteWord<EPL>::type w[BY];
 #pragma unroll
             for (int y = 0; y < BY; ++y) {
                 const int c = r * BY + y;
-                if (c < p) load_bytes<T>(in + (int64_t)c * chunk_offset + 32 + e0 + v * N, b[y]);
+                if (c < p) w[y] = load_payload<EPL>(base + (int64_t)c * chunk_offset + g * EPL);
             }
 #pragma unroll
             for (int y = 0; y < BY; ++y) {
                 const int c = r * BY + y;
                 if (c >= p) break;
-                const QParams q = qp[c];
 #pragma unroll
-                for (int i = 0; i < N; ++i) s[i][y] = s[i][y] + as_stored<T>(dequant(b[y][i], q));
+                for (int i = 0; i < EPL; ++i) s[i][y] = s[i][y] + lut[c][payload_byte<EPL>(w[y], i)];
             }
         }
-        float o[N];
 #pragma unroll
-        for (int i = 0; i < N; ++i) {
-            tree_finish<BY>(s[i]);
-            o[i] = AVG ? s[i][0] / pf : s[i][0];
-        }
-        const uint4 packed = pack16<T>(o);
-        *reinterpret_cast<uint4*>(out + v * N) = packed;
-        if constexpr (PARTIALS) {
-            // min/max of the values as stored in T (what the requantiser reads back)
-            float st[N];
-            unpack16<T>(packed, st);
+        for (int q = 0; q < EPL / N; ++q) {
+            float o[N];
 #pragma unroll
             for (int i = 0; i < N; ++i) {
-                const int32_t k = f2key(st[i]);
-                if (st[i] == st[i]) {
+                tree_finish<BY>(s[q * N + i]);
+                o[i] = AVG ? s[q * N + i][0] / pf : s[q * N + i][0];
+            }
+            const uint4 packed = pack16<T>(o);
+            *reinterpret_cast<uint4*>(out + g * EPL + q * N) = packed;
+            if constexpr (PARTIALS) {
+                // min/max of the values as stored in T (what the requantiser reads back)
+                float st[N];
+                unpack16<T>(packed, st);
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    const int32_t k = f2key(st[i]);  // NaN wraps to a huge key in both spaces
                     lo = min(lo, min_space_key(k));
                     hi = min(hi, max_space_key(k));
                 }
             }
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x < cs - nvec * N) {  // ragged tail
-        const int64_t j = nvec * N + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < cs - ngrp * EPL) {  // ragged tail (< EPL elements)
+        const int64_t j = ngrp * EPL + threadIdx.x;
         float s[BY];
 #pragma unroll
         for (int y = 0; y < BY; ++y) s[y] = 0.0f;
         for (int c = 0; c < p; ++c) {
             const int y = c % BY;
-            s[y] = s[y] + as_stored<T>(dequant(in[(int64_t)c * chunk_offset + 32 + e0 + j], qp[c]));
+            s[y] = s[y] + lut[c][base[(int64_t)c * chunk_offset + j]];
         }
         tree_finish<BY>(s);
         const S o = T::from_f(AVG ? s[0] / pf : s[0]);
         out[j] = o;
         if constexpr (PARTIALS) {
-            const float st = T::to_f(o);
-            if (st == st) {
-                const int32_t k = f2key(st);
-                lo = min(lo, min_space_key(k));
-                hi = min(hi, max_space_key(k));
-            }
+            const int32_t k = f2key(T::to_f(o));
+            lo = min(lo, min_space_key(k));
+            hi = min(hi, max_space_key(k));
         }
     }
     if constexpr (PARTIALS) {
@@ -235,24 +264,36 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
     }
 }
 
-template <typename T, int BY, bool AVG>
+template <typename T, int BY, bool AVG, int EPL>
 static void launch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, int p, typename T::storage* out,
                          uint2* partials, int blocks, hipStream_t s) {
     if (partials)
-        hipLaunchKernelGGL((dequant_reduce_kernel<T, BY, AVG, true>), dim3(blocks), dim3(kBlock), 0, s, in, co,
+        hipLaunchKernelGGL((dequant_reduce_kernel<T, BY, AVG, true, EPL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
                            e0, cs, p, out, partials);
     else
-        hipLaunchKernelGGL((dequant_reduce_kernel<T, BY, AVG, false>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                           e0, cs, p, out, partials);
+        hipLaunchKernelGGL((dequant_reduce_kernel<T, BY, AVG, false, EPL>), dim3(blocks), dim3(kBlock), 0, s, in,
+                           co, e0, cs, p, out, partials);
 }
 
+// wide: segments 16-B aligned -> 16 B per segment per lane (8 B at BY = 8 to
+// bound the accumulators at 64 VGPRs); narrow: one output vector's N bytes
 template <typename T, bool AVG>
 static void dispatch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, int p, typename T::storage* out,
-                           uint2* partials, int blocks, hipStream_t s) {
+                           uint2* partials, int blocks, bool wide, hipStream_t s) {
+    constexpr int N = Vec<T>::N;
     switch (reduce_by(p)) {  // p <= kMaxFusedChunks (16) keeps BY <= 8
-        case 2: launch_fused<T, 2, AVG>(in, co, e0, cs, p, out, partials, blocks, s); break;
-        case 4: launch_fused<T, 4, AVG>(in, co, e0, cs, p, out, partials, blocks, s); break;
-        default: launch_fused<T, 8, AVG>(in, co, e0, cs, p, out, partials, blocks, s); break;
+        case 2:
+            if (wide) launch_fused<T, 2, AVG, 16>(in, co, e0, cs, p, out, partials, blocks, s);
+            else launch_fused<T, 2, AVG, N>(in, co, e0, cs, p, out, partials, blocks, s);
+            break;
+        case 4:
+            if (wide) launch_fused<T, 4, AVG, 16>(in, co, e0, cs, p, out, partials, blocks, s);
+            else launch_fused<T, 4, AVG, N>(in, co, e0, cs, p, out, partials, blocks, s);
+            break;
+        default:
+            if (wide) launch_fused<T, 8, AVG, 8>(in, co, e0, cs, p, out, partials, blocks, s);
+            else launch_fused<T, 8, AVG, N>(in, co, e0, cs, p, out, partials, blocks, s);
+            break;
     }
 }
 
@@ -276,8 +317,9 @@ int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void*
     S* o = static_cast<S*>(out) + e0;
     const bool aligned = ((uintptr_t)o % 16 == 0) && (((uintptr_t)in + 32 + e0) % N == 0) && (co % N == 0);
     if (!aligned) return BAGUA_ERR_UNSUPPORTED;  // caller falls back to decompress + reduce
-    if (average) dispatch_fused<T, true>(in, co, e0, e1 - e0, p, o, partials, blocks, s);
-    else dispatch_fused<T, false>(in, co, e0, e1 - e0, p, o, partials, blocks, s);
+    const bool wide = (((uintptr_t)in + 32 + e0) % 16 == 0) && (co % 16 == 0);
+    if (average) dispatch_fused<T, true>(in, co, e0, e1 - e0, p, o, partials, blocks, wide, s);
+    else dispatch_fused<T, false>(in, co, e0, e1 - e0, p, o, partials, blocks, wide, s);
     return check_launch();
 }
 
