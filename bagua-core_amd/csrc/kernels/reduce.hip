@@ -135,39 +135,24 @@ static int reduce_impl(void* x, int cs, int p, int target, int average, hipStrea
 }
 
 // ---------------------------------------------- fused dequantise + reduce --
-// EPL payload bytes of one segment as one load (4, 8 or 16 B)
-template <int EPL>
-struct ByteWord;
-template <> struct ByteWord<4> { using type = uint32_t; };
-template <> struct ByteWord<8> { using type = uint2; };
-template <> struct ByteWord<16> { using type = uint4; };
-
-template <int EPL>
-__device__ __forceinline__ typename ByteWord<EPL>::type load_payload(const uint8_t* p) {
-    if constexpr (EPL == 4) return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
-    else if constexpr (EPL == 8) return nt_load8(p);
-    else return nt_load16(p);
-}
-template <int EPL>
-__device__ __forceinline__ uint32_t payload_byte(const typename ByteWord<EPL>::type& w, int i) {
-    uint32_t d;
-    if constexpr (EPL == 4) d = w;
-    else if constexpr (EPL == 8) d = (i < 4) ? w.x : w.y;
-    else d = (i < 4) ? w.x : (i < 8) ? w.y : (i < 12) ? w.z : w.w;
-    return (d >> (8 * (i & 3))) & 0xffu;
+// Each lane reduces Q output vectors per step, taken at block stride so every
+// load (N payload bytes of one segment) and every 16-B store of a wave is
+// contiguous; Q = 64 / (N * BY) keeps BY x Q x N = 64 payload bytes in flight
+// per lane (and 64 accumulators) for every p.  Summation follows the
+// reference's tree order (block_y_reduce, K:171-194).
+template <typename T, int BY>
+constexpr int fused_q() {
+    return (64 / (Vec<T>::N * BY)) < 1 ? 1 : 64 / (Vec<T>::N * BY);
 }
 
-// Each lane reduces EPL consecutive elements per step: one EPL-byte load per
-// segment (16 B where the segments allow it, so a lane keeps BY x 16 B in
-// flight), summed in the reference's tree order (block_y_reduce, K:171-194).
-template <typename T, int BY, bool AVG, bool PARTIALS, int EPL>
+template <typename T, int BY, bool AVG, bool PARTIALS>
 __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
     const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t e0, int64_t cs, int p,
     typename T::storage* __restrict__ out, uint2* __restrict__ partials) {
     // reduces elements [e0, e0 + cs) of the chunk (`out` points at element e0)
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
-    static_assert(EPL % N == 0, "whole output vectors per lane");
+    constexpr int Q = fused_q<T, BY>();
     __shared__ QParams qp[kMaxFusedChunks];
     for (int c = threadIdx.x; c < p; c += kBlock) {
         const uint8_t* seg = in + (int64_t)c * chunk_offset;
@@ -184,40 +169,64 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
     __syncthreads();
     const float pf = (float)p;
     uint32_t lo = min_space(T::init_max()), hi = max_space(-T::init_max());
-    // fast path: every segment's payload EPL-byte aligned and out 16-B aligned (checked on host)
-    const int64_t ngrp = cs / EPL;
+    // fast path: every segment's payload N-byte aligned and out 16-B aligned (checked on host)
+    const int64_t nvec = cs / N;
     const uint8_t* base = in + 32 + e0;
-    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < ngrp; g += (int64_t)gridDim.x * kBlock) {
-        float s[EPL][BY];
+    for (int64_t tile = (int64_t)blockIdx.x * kBlock * Q; tile < nvec; tile += (int64_t)gridDim.x * kBlock * Q) {
+        const bool full = tile + (int64_t)kBlock * Q <= nvec;
+        float s[Q][N][BY];
 #pragma unroll
-        for (int i = 0; i < EPL; ++i)
+        for (int q = 0; q < Q; ++q)
 #pragma unroll
-            for (int y = 0; y < BY; ++y) s[i][y] = 0.0f;
+            for (int i = 0; i < N; ++i)
+#pragma unroll
+                for (int y = 0; y < BY; ++y) s[q][i][y] = 0.0f;
         for (int r = 0; r * BY < p; ++r) {
-            typename ByteWord<EPL>::type w[BY];
+            typename Vec<T>::out_bytes w[BY][Q];
+            if (full) {  // unconditional loads: all BY x Q in flight before the first use
 #pragma unroll
-            for (int y = 0; y < BY; ++y) {
-                const int c = r * BY + y;
-                if (c < p) w[y] = load_payload<EPL>(base + (int64_t)c * chunk_offset + g * EPL);
+                for (int y = 0; y < BY; ++y)
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) {
+                        const int c = r * BY + y < p ? r * BY + y : p - 1;
+                        w[y][q] = load_word<T>(base + (int64_t)c * chunk_offset +
+                                               (tile + q * kBlock + threadIdx.x) * N);
+                    }
+            } else {
+#pragma unroll
+                for (int y = 0; y < BY; ++y)
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) {
+                        const int64_t v = tile + q * kBlock + threadIdx.x;
+                        const int c = r * BY + y;
+                        if (c < p && v < nvec) w[y][q] = load_word<T>(base + (int64_t)c * chunk_offset + v * N);
+                    }
             }
 #pragma unroll
             for (int y = 0; y < BY; ++y) {
                 const int c = r * BY + y;
                 if (c >= p) break;
 #pragma unroll
-                for (int i = 0; i < EPL; ++i) s[i][y] = s[i][y] + lut[c][payload_byte<EPL>(w[y], i)];
+                for (int q = 0; q < Q; ++q) {
+                    uint32_t b[N];
+                    split_bytes<T>(w[y][q], b);
+#pragma unroll
+                    for (int i = 0; i < N; ++i) s[q][i][y] = s[q][i][y] + lut[c][b[i]];
+                }
             }
         }
 #pragma unroll
-        for (int q = 0; q < EPL / N; ++q) {
+        for (int q = 0; q < Q; ++q) {
+            const int64_t v = tile + q * kBlock + threadIdx.x;
+            if (!full && v >= nvec) continue;
             float o[N];
 #pragma unroll
             for (int i = 0; i < N; ++i) {
-                tree_finish<BY>(s[q * N + i]);
-                o[i] = AVG ? s[q * N + i][0] / pf : s[q * N + i][0];
+                tree_finish<BY>(s[q][i]);
+                o[i] = AVG ? s[q][i][0] / pf : s[q][i][0];
             }
             const uint4 packed = pack16<T>(o);
-            *reinterpret_cast<uint4*>(out + g * EPL + q * N) = packed;
+            *reinterpret_cast<uint4*>(out + v * N) = packed;
             if constexpr (PARTIALS) {
                 // min/max of the values as stored in T (what the requantiser reads back)
                 float st[N];
@@ -231,8 +240,8 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
             }
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x < cs - ngrp * EPL) {  // ragged tail (< EPL elements)
-        const int64_t j = ngrp * EPL + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < cs - nvec * N) {  // ragged tail (< N elements)
+        const int64_t j = nvec * N + threadIdx.x;
         float s[BY];
 #pragma unroll
         for (int y = 0; y < BY; ++y) s[y] = 0.0f;
@@ -264,36 +273,24 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
     }
 }
 
-template <typename T, int BY, bool AVG, int EPL>
+template <typename T, int BY, bool AVG>
 static void launch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, int p, typename T::storage* out,
                          uint2* partials, int blocks, hipStream_t s) {
     if (partials)
-        hipLaunchKernelGGL((dequant_reduce_kernel<T, BY, AVG, true, EPL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                           e0, cs, p, out, partials);
+        hipLaunchKernelGGL((dequant_reduce_kernel<T, BY, AVG, true>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
+                           cs, p, out, partials);
     else
-        hipLaunchKernelGGL((dequant_reduce_kernel<T, BY, AVG, false, EPL>), dim3(blocks), dim3(kBlock), 0, s, in,
-                           co, e0, cs, p, out, partials);
+        hipLaunchKernelGGL((dequant_reduce_kernel<T, BY, AVG, false>), dim3(blocks), dim3(kBlock), 0, s, in, co,
+                           e0, cs, p, out, partials);
 }
 
-// wide: segments 16-B aligned -> 16 B per segment per lane (8 B at BY = 8 to
-// bound the accumulators at 64 VGPRs); narrow: one output vector's N bytes
 template <typename T, bool AVG>
 static void dispatch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, int p, typename T::storage* out,
-                           uint2* partials, int blocks, bool wide, hipStream_t s) {
-    constexpr int N = Vec<T>::N;
+                           uint2* partials, int blocks, hipStream_t s) {
     switch (reduce_by(p)) {  // p <= kMaxFusedChunks (16) keeps BY <= 8
-        case 2:
-            if (wide) launch_fused<T, 2, AVG, 16>(in, co, e0, cs, p, out, partials, blocks, s);
-            else launch_fused<T, 2, AVG, N>(in, co, e0, cs, p, out, partials, blocks, s);
-            break;
-        case 4:
-            if (wide) launch_fused<T, 4, AVG, 16>(in, co, e0, cs, p, out, partials, blocks, s);
-            else launch_fused<T, 4, AVG, N>(in, co, e0, cs, p, out, partials, blocks, s);
-            break;
-        default:
-            if (wide) launch_fused<T, 8, AVG, 8>(in, co, e0, cs, p, out, partials, blocks, s);
-            else launch_fused<T, 8, AVG, N>(in, co, e0, cs, p, out, partials, blocks, s);
-            break;
+        case 2: launch_fused<T, 2, AVG>(in, co, e0, cs, p, out, partials, blocks, s); break;
+        case 4: launch_fused<T, 4, AVG>(in, co, e0, cs, p, out, partials, blocks, s); break;
+        default: launch_fused<T, 8, AVG>(in, co, e0, cs, p, out, partials, blocks, s); break;
     }
 }
 
@@ -317,9 +314,8 @@ int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void*
     S* o = static_cast<S*>(out) + e0;
     const bool aligned = ((uintptr_t)o % 16 == 0) && (((uintptr_t)in + 32 + e0) % N == 0) && (co % N == 0);
     if (!aligned) return BAGUA_ERR_UNSUPPORTED;  // caller falls back to decompress + reduce
-    const bool wide = (((uintptr_t)in + 32 + e0) % 16 == 0) && (co % 16 == 0);
-    if (average) dispatch_fused<T, true>(in, co, e0, e1 - e0, p, o, partials, blocks, wide, s);
-    else dispatch_fused<T, false>(in, co, e0, e1 - e0, p, o, partials, blocks, wide, s);
+    if (average) dispatch_fused<T, true>(in, co, e0, e1 - e0, p, o, partials, blocks, s);
+    else dispatch_fused<T, false>(in, co, e0, e1 - e0, p, o, partials, blocks, s);
     return check_launch();
 }
 
