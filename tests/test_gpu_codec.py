@@ -291,3 +291,29 @@ def test_full_size_256mib_parity(bc, oracle_c):
     bound = 0.5 * (float(xh.max()) - float(xh.min()) + 1e-7) / 255 * (1 + 1e-4) + 2 * float(np.spacing(np.float32(
         np.abs(xh).max())))
     assert float(np.abs(dw.astype(np.float64) - xh).max()) <= bound
+
+
+def test_maximum_size_bucket_parity(bc, oracle_c):
+    """The largest bucket the reference's int32 ABI can describe (K:573-691 take
+    `int` element counts): n = 2^31 - 32 fp32 elements (8 GiB) in p = 4 chunks,
+    so every 64-bit offset path of the kernels is exercised.  Payload, headers
+    and the decoded tensor must equal the C oracle bit-for-bit."""
+    n, p = (1 << 31) - 32, 4
+    g = torch.Generator(device="cuda").manual_seed(31)
+    x = torch.randn(n, device="cuda", generator=g)
+    x[n - 1] = 7.5  # the maximum sits in the very last element of the last chunk
+    t = bc.BaguaTensorPy(x, "max_bucket")
+    comp = t.compress("MinMaxUInt8", p, -1)
+    got = comp.to_numpy_u8()
+    xh = x.cpu().numpy()
+    want = oracle_c.compress_minmax_u8(xh, F32, p)
+    assert got.size == want.size
+    assert np.array_equal(got, want)
+    del got
+    out = torch.empty_like(x)
+    bc.BaguaTensorPy(out, "o").decompress_from("MinMaxUInt8", p, comp)
+    del x
+    dw = np.empty_like(xh)
+    del xh
+    oracle_c.decompress_minmax_u8(want, p, dw, F32)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), dw.view(np.uint32))
