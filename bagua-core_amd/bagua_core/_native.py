@@ -57,6 +57,7 @@ def _sig(lib, name, restype, argtypes):
 KERNEL_SIGNATURES = {
     "bagua_status_string": (ctypes.c_char_p, [_i32]),
     "bagua_last_hip_error": (_i32, []),
+    "bagua_time_next_kernel": (_i32, [_vp, _vp]),
     "bagua_minmax_u8_compressed_bytes": (_sz, [_i32, _i32, _i32]),
     "bagua_minmax_u8_workspace_bytes": (_sz, [_i32, _i32]),
     "bagua_minmax_u8_compress": (_i32, [_i32, _vp, _i32, _i32, _i32, _vp, _sz, _vp, _sz, _i32, _vp]),

@@ -165,7 +165,7 @@ static int mix_impl(void* t, const void* l, const void* r, const void* w, int n,
     if (!aligned16(t) || !aligned16(l) || !aligned16(r) || !aligned16(w)) return BAGUA_ERR_UNSUPPORTED;
     const int nblk = ws ? minmax_partials_blocks(n, Vec<T>::N, 1, ws_bytes) : 0;
     if (nblk < 1) return BAGUA_ERR_WORKSPACE;
-    hipLaunchKernelGGL(ring_mix_kernel<T>, dim3(nblk), dim3(kBlock), 0, s, static_cast<S*>(t),
+    launch(ring_mix_kernel<T>, dim3(nblk), dim3(kBlock), 0, s, static_cast<S*>(t),
                        static_cast<const S*>(l), static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13,
                        f53, static_cast<uint2*>(ws));
     return check_launch();
@@ -184,7 +184,7 @@ static int apply_impl(const uint8_t* mine, const uint8_t* from_left, const uint8
     int64_t blocks = ((int64_t)n / N + kBlock - 1) / kBlock;
     if (blocks > 2 * kTargetBlocks) blocks = 2 * kTargetBlocks;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(ring_apply_kernel<T>, dim3(blocks), dim3(kBlock), 0, s, mine, from_left, from_right,
+    launch(ring_apply_kernel<T>, dim3(blocks), dim3(kBlock), 0, s, mine, from_left, from_right,
                        static_cast<S*>(t), static_cast<S*>(w), static_cast<S*>(l), static_cast<S*>(r), (int64_t)n);
     return check_launch();
 }

@@ -69,10 +69,10 @@ static int launch_binary(void* x, const void* y, int n, float f, hipStream_t s) 
     if (blocks > kTargetBlocks) blocks = kTargetBlocks;
     if (blocks < 1) blocks = 1;
     if (vec)
-        hipLaunchKernelGGL((binary_kernel<T, OP, true>), dim3(blocks), dim3(kBlock), 0, s, static_cast<S*>(x),
+        launch((binary_kernel<T, OP, true>), dim3(blocks), dim3(kBlock), 0, s, static_cast<S*>(x),
                            static_cast<const S*>(y), (int64_t)n, f);
     else
-        hipLaunchKernelGGL((binary_kernel<T, OP, false>), dim3(blocks), dim3(kBlock), 0, s, static_cast<S*>(x),
+        launch((binary_kernel<T, OP, false>), dim3(blocks), dim3(kBlock), 0, s, static_cast<S*>(x),
                            static_cast<const S*>(y), (int64_t)n, f);
     return check_launch();
 }
@@ -152,7 +152,7 @@ void async_model_average_host(float* tensor, const float* reduced_tensor_copy, c
     if (N <= 0) return;
     int blocks = (N + kBlock - 1) / kBlock;
     if (blocks > kTargetBlocks) blocks = kTargetBlocks;
-    hipLaunchKernelGGL(async_model_average_kernel, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+    launch(async_model_average_kernel, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
                        tensor, reduced_tensor_copy, tensor_copy, nranks, N);
     V1(check_launch());
 }

@@ -1,6 +1,7 @@
 // launch_util.hpp — host-side launch helpers shared by the kernel TUs.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -15,6 +16,22 @@ constexpr int kTargetBlocks = 2048;
 
 // last hipError_t seen by a launcher on this thread (bagua_last_hip_error)
 extern thread_local int g_last_hip_error;
+
+// Bench instrumentation (bagua_time_next_kernel): when armed, the next kernel
+// this library launches on this thread records `start`/`stop` at its own start
+// and end (hipExtLaunchKernel), so its duration excludes dispatch overhead.
+struct KernelTiming {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local KernelTiming g_kernel_timing;
+
+// every kernel of the library is launched through here
+template <typename F, typename... Args>
+inline void launch(F kernel, const dim3& grid, const dim3& block, uint32_t shmem, hipStream_t s, Args... args) {
+    const KernelTiming t = g_kernel_timing;
+    g_kernel_timing = KernelTiming{};
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, t.start, t.stop, 0u, args...);
+}
 
 inline int check_launch() {
     hipError_t e = hipGetLastError();

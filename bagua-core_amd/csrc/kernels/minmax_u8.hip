@@ -332,10 +332,10 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
     if (nblk < 1) return BAGUA_ERR_WORKSPACE;
     uint2* partials = static_cast<uint2*>(ws);
     if (stages & 1)
-        hipLaunchKernelGGL(minmax_partials_kernel<T>, dim3(nblk, nact), dim3(kBlock), 0, s,
+        launch(minmax_partials_kernel<T>, dim3(nblk, nact), dim3(kBlock), 0, s,
                            static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, partials);
     if (stages & 2)
-        hipLaunchKernelGGL((minmax_quantize_kernel<T, true>), dim3(blocks_for(e1 - e0, Vec<T>::N, nact), nact),
+        launch((minmax_quantize_kernel<T, true>), dim3(blocks_for(e1 - e0, Vec<T>::N, nact), nact),
                            dim3(kBlock), 0, s, static_cast<const S*>(input), (int64_t)in_num_elem,
                            (int64_t)cs, (int64_t)e0, (int64_t)e1, target, partials, nblk, out, chunk_offset,
                            (int64_t)out_bytes, p);
@@ -363,7 +363,7 @@ static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs
     uint2* partials = static_cast<uint2*>(ws);
     int rc = dequant_reduce_impl<T>(recv, recv_bytes, cs, p, chunk, average, partials, blocks, s, 0, cs);
     if (rc) return rc;
-    hipLaunchKernelGGL((minmax_quantize_kernel<T, true>), dim3(blocks_for(cs, Vec<T>::N, 1), 1), dim3(kBlock), 0, s,
+    launch((minmax_quantize_kernel<T, true>), dim3(blocks_for(cs, Vec<T>::N, 1), 1), dim3(kBlock), 0, s,
                        static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, (int64_t)0, (int64_t)cs, target,
                        partials, blocks, out, chunk_offset, (int64_t)out_bytes, p);
     return check_launch();
@@ -411,7 +411,7 @@ static int requantize_pieces_impl(const void* tensor, int cs, int p, uint8_t* ou
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     const int blocks = piece_blocks(cs, pieces, Vec<T>::N);
     if (!ws || ws_bytes < (size_t)pieces * blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
-    hipLaunchKernelGGL((minmax_quantize_kernel<T, true>), dim3(blocks_for(cs, Vec<T>::N, 1), 1), dim3(kBlock), 0, s,
+    launch((minmax_quantize_kernel<T, true>), dim3(blocks_for(cs, Vec<T>::N, 1), 1), dim3(kBlock), 0, s,
                        static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, (int64_t)0, (int64_t)cs, target,
                        static_cast<const uint2*>(ws), pieces * blocks, out, chunk_offset, (int64_t)out_bytes, p);
     return check_launch();
@@ -425,7 +425,7 @@ static int decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p, vo
     if (p <= 0 || p > 65535 || cs < 0 || !in || !out || e0 < 0 || e1 < e0 || e1 > cs) return BAGUA_ERR_INVALID_ARG;
     const int64_t chunk_offset = (int64_t)(in_bytes / (size_t)p);  // K:566
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
-    hipLaunchKernelGGL(minmax_dequantize_kernel<T>,
+    launch(minmax_dequantize_kernel<T>,
                        dim3(blocks_for(e1 - e0, Vec<T>::N, p, kSubtiles, kDequantBlocks), p), dim3(kBlock), 0,
                        s, in, chunk_offset, (int64_t)cs, (int64_t)e0, (int64_t)e1, static_cast<S*>(out));
     return check_launch();

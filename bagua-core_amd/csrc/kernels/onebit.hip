@@ -322,10 +322,10 @@ static int ob_compress_impl(const void* input, int in_num_elem, int cs, int p, u
     if (((uintptr_t)out + 32) % 4 || co % 4) return BAGUA_ERR_INVALID_ARG;  // bit tiles are written as dwords
     float* partials = static_cast<float*>(ws);
     if (tiles > 0)
-        hipLaunchKernelGGL(onebit_encode_kernel<T>, dim3(ob_blocks(tiles, nact), nact), dim3(kBlock), 0, s,
+        launch(onebit_encode_kernel<T>, dim3(ob_blocks(tiles, nact), nact), dim3(kBlock), 0, s,
                            static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, out, co, partials,
                            tiles);
-    hipLaunchKernelGGL(onebit_finalize_kernel, dim3(nact), dim3(kObFinalizeThreads), 0, s, partials, tiles,
+    launch(onebit_finalize_kernel, dim3(nact), dim3(kObFinalizeThreads), 0, s, partials, tiles,
                        (int64_t)in_num_elem, (int64_t)cs, target, out, co, (int64_t)out_bytes, p);
     return check_launch();
 }
@@ -339,7 +339,7 @@ static int ob_decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p,
     if (co < 32 + tiles * kObTileBytes) return BAGUA_ERR_INVALID_ARG;
     if (((uintptr_t)in + 32) % 4 || co % 4) return BAGUA_ERR_INVALID_ARG;
     if (tiles == 0) return BAGUA_OK;
-    hipLaunchKernelGGL(onebit_decode_kernel<T>, dim3(ob_blocks(tiles, p), p), dim3(kBlock), 0, s, in, co,
+    launch(onebit_decode_kernel<T>, dim3(ob_blocks(tiles, p), p), dim3(kBlock), 0, s, in, co,
                        (int64_t)cs, static_cast<S*>(out));
     return check_launch();
 }

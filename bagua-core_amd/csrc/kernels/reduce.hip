@@ -106,12 +106,12 @@ static void launch_reduce(typename T::storage* x, int64_t cs, int p, int target,
     if (blocks < 1) blocks = 1;
     if constexpr (kVecFits) {
         if (vec) {
-            hipLaunchKernelGGL((reduce_chunks_kernel<T, BY, AVG, true>), dim3(blocks), dim3(kBlock), 0, s, x, cs, p,
+            launch((reduce_chunks_kernel<T, BY, AVG, true>), dim3(blocks), dim3(kBlock), 0, s, x, cs, p,
                                target);
             return;
         }
     }
-        hipLaunchKernelGGL((reduce_chunks_kernel<T, BY, AVG, false>), dim3(blocks), dim3(kBlock), 0, s, x, cs, p, target);
+        launch((reduce_chunks_kernel<T, BY, AVG, false>), dim3(blocks), dim3(kBlock), 0, s, x, cs, p, target);
 }
 
 template <typename T, bool AVG>
@@ -277,10 +277,10 @@ template <typename T, int BY, bool AVG>
 static void launch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, int p, typename T::storage* out,
                          uint2* partials, int blocks, hipStream_t s) {
     if (partials)
-        hipLaunchKernelGGL((dequant_reduce_kernel<T, BY, AVG, true>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
+        launch((dequant_reduce_kernel<T, BY, AVG, true>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
                            cs, p, out, partials);
     else
-        hipLaunchKernelGGL((dequant_reduce_kernel<T, BY, AVG, false>), dim3(blocks), dim3(kBlock), 0, s, in, co,
+        launch((dequant_reduce_kernel<T, BY, AVG, false>), dim3(blocks), dim3(kBlock), 0, s, in, co,
                            e0, cs, p, out, partials);
 }
 

@@ -4,6 +4,7 @@
 
 namespace bagua {
 thread_local int g_last_hip_error = 0;
+thread_local KernelTiming g_kernel_timing;
 }
 
 extern "C" {
@@ -20,5 +21,12 @@ const char* bagua_status_string(int status) {
 }
 
 int bagua_last_hip_error(void) { return bagua::g_last_hip_error; }
+
+int bagua_time_next_kernel(void* start_event, void* stop_event) {
+    if ((start_event == nullptr) != (stop_event == nullptr)) return BAGUA_ERR_INVALID_ARG;
+    bagua::g_kernel_timing.start = static_cast<hipEvent_t>(start_event);
+    bagua::g_kernel_timing.stop = static_cast<hipEvent_t>(stop_event);
+    return BAGUA_OK;
+}
 
 }  // extern "C"

@@ -98,12 +98,13 @@ def bench_codec(args, onebit: bool = False):
     xp, yp, cp, wp = x.data_ptr(), y.data_ptr(), comp.data_ptr(), ws.data_ptr()
 
     if onebit:
-        names = ["onebit_encode+finalize", "onebit_decode"]
+        # the compress call launches encode then finalize; the timing hook times its first kernel
+        names = ["onebit_encode_kernel", "onebit_decode_kernel"]
 
         def launches():
             return [lambda: K.bagua_onebit_compress(dcode, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
                     lambda: K.bagua_onebit_decompress(dcode, cp, S, n, p, yp, sp)]
-        alg = [esz * n + n // 8 + 32, n // 8 + 32 + esz * n]
+        alg = [esz * n + n // 8 + 4 * ((n + 1023) // 1024), n // 8 + 32 + esz * n]  # + per-tile |x| partials
     else:
         names = ["minmax_partials_kernel", "minmax_quantize_kernel", "minmax_dequantize_kernel"]
 
@@ -122,35 +123,41 @@ def bench_codec(args, onebit: bool = False):
             if rc:
                 raise RuntimeError(f"kernel launch failed: {N.STATUS.get(rc, rc)}")
 
-    # warmup; its last steps carry an event after every launch to find the
-    # dominant kernel (events between kernels perturb the cache state, so the
-    # timed region below only brackets that one kernel)
+    # Kernel durations come from HIP events that the kernels themselves record
+    # at their start and end (bagua_time_next_kernel -> hipExtLaunchKernel), so
+    # they exclude dispatch overhead and agree with rocprofv3's kernel trace.
+    def kernel_events(count):
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(count)]
+        for a, b in evs:  # torch creates the HIP events on first record
+            a.record(stream)
+            b.record(stream)
+        return evs
+
+    # warmup; the last steps time every kernel to find the dominant one
     nprof = min(5, max(1, args.warmup))
     for _ in range(max(0, args.warmup - nprof)):
         step()
-    pev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(calls) + 1)] for _ in range(nprof)]
-    for k in range(nprof):
-        pev[k][0].record(stream)
-        for i, c in enumerate(calls):
-            c()
-            pev[k][i + 1].record(stream)
+    pev = [kernel_events(len(calls)) for _ in range(nprof)]
     torch.cuda.synchronize()
-    per = [sum(pev[k][i].elapsed_time(pev[k][i + 1]) for k in range(nprof)) / nprof for i in range(len(calls))]
+    for k in range(nprof):
+        for i, c in enumerate(calls):
+            N.check(K.bagua_time_next_kernel(pev[k][i][0].cuda_event, pev[k][i][1].cuda_event), "timing hook")
+            c()
+    torch.cuda.synchronize()
+    per = [sum(pev[k][i][0].elapsed_time(pev[k][i][1]) for k in range(nprof)) / nprof for i in range(len(calls))]
     dom = max(range(len(calls)), key=lambda i: per[i])
-    # timed region: K steps, wall clock between synchronisations; HIP events on
-    # the launch stream bracket the dominant kernel of every step
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # timed region: K steps, wall clock between synchronisations; the dominant
+    # kernel of every step records its own start/stop events
+    ev = kernel_events(args.steps)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         for i, c in enumerate(calls):
             if i == dom:
-                ev[k][0].record(stream)
+                K.bagua_time_next_kernel(ev[k][0].cuda_event, ev[k][1].cuda_event)
             rc = c()
             if rc:
                 raise RuntimeError(f"kernel launch failed: {N.STATUS.get(rc, rc)}")
-            if i == dom:
-                ev[k][1].record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     ms = wall * 1e3 / args.steps
@@ -170,7 +177,8 @@ def bench_codec(args, onebit: bool = False):
         "step_roofline": {"alg_bytes": step_alg, "wall_us": round(ms * 1e3, 2),
                           "achieved_gbs": round(step_alg / (ms * 1e-3) / 1e9, 1),
                           "frac": round(step_alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-        "per_kernel_note": "dominant kernel: timed-region events; others: warmup events between launches",
+        "per_kernel_note": "kernel-recorded HIP events (hipExtLaunchKernel); dominant kernel over the timed region, "
+                           "others over the last warmup steps",
         "encode_gib_s": round(esz * n / (sum(per[:-1]) * 1e-3) / GiB, 1),
         "decode_gib_s": round(esz * n / (per[-1] * 1e-3) / GiB, 1),
     }
@@ -398,16 +406,20 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     names = ["minmax_partials_kernel", "minmax_quantize_kernel", "minmax_dequantize_kernel"]
     alg = [4 * n, 5 * n + 32 * world, 5 * n + 32 * world]
     reps = 5
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(reps)]
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+          for _ in range(reps)]
+    for row in ev:  # torch creates the HIP events on first record
+        for a, b in row:
+            a.record(st)
+            b.record(st)
     for c in calls:
         c()
     for k in range(reps):
-        ev[k][0].record(st)
-        for i, c in enumerate(calls):
+        for i, c in enumerate(calls):  # kernel-recorded start/stop events (hipExtLaunchKernel)
+            N.check(K.bagua_time_next_kernel(ev[k][i][0].cuda_event, ev[k][i][1].cuda_event), "timing hook")
             c()
-            ev[k][i + 1].record(st)
     torch.cuda.synchronize()
-    per = [sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(reps)) / reps for i in range(3)]
+    per = [sum(ev[k][i][0].elapsed_time(ev[k][i][1]) for k in range(reps)) / reps for i in range(3)]
     dom = max(range(3), key=lambda i: per[i])
     achieved = alg[dom] / (per[dom] * 1e-3) / 1e9
     roof = {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -46,6 +46,11 @@ typedef enum {
 
 const char* bagua_status_string(int status);
 int bagua_last_hip_error(void);
+/* Measurement hook: the next kernel this library launches on the calling thread
+ * records the two hipEvent_t (created with timing) at its own start and end
+ * (hipExtLaunchKernel), so hipEventElapsedTime gives the kernel's duration
+ * without dispatch overhead.  Both NULL disarms.  One-shot. */
+int bagua_time_next_kernel(void* start_event, void* stop_event);
 
 /* ======================================================================== */
 /* v2 — MinMax-UInt8 codec (format: datatypes/mod.rs:669-704, K:455-500)     */

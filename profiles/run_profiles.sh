@@ -1,0 +1,29 @@
+#!/usr/bin/env bash
+# Regenerates the committed profiles on a GPU box (gpurun):
+#   bash profiles/run_profiles.sh r01
+# 1. kernel trace + stats of the default bench (config 2) and of the 1-bit bench
+# 2. two SEPARATE counter passes (FETCH_SIZE, WRITE_SIZE) of the same bench
+#    (MI355X_MICROARCH.md: never combined with tracing), summarised by
+#    collect_pmc.py into <round>_pmc_traffic.json
+# Raw output stays under gpurun_out/prof; the summaries are copied to profiles/.
+set -euo pipefail
+R=${1:-r01}
+OUT=gpurun_out/prof
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+BENCH=(bench.py --steps 30 --warmup 5 --no-cpu-baseline)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o codec -- \
+    python3 "${BENCH[@]}" > "$OUT/codec_under_rocprof.json"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_ob" -o onebit -- \
+    python3 "${BENCH[@]}" --workload onebit > "$OUT/onebit_under_rocprof.json"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > /dev/null
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > /dev/null
+# python3 profiles/collect_pmc.py "$OUT/fetch" "$OUT/write" "profiles/${R}_pmc_traffic.json"
+# (run locally on the merged gpurun_out/: only gpurun_out/ returns from the box)
+# cp "$(find "$OUT/trace" -name '*kernel_stats.csv' | head -1)" "profiles/${R}_bench_n1_kernel_stats.csv"
+# (run locally on the merged gpurun_out/: only gpurun_out/ returns from the box)
+# cp "$(find "$OUT/trace_ob" -name '*kernel_stats.csv' | head -1)" "profiles/${R}_onebit_kernel_stats.csv"
+# cp "$OUT/codec_under_rocprof.json" "profiles/${R}_bench_n1_under_rocprof.json"
+echo "profiles written for $R"
