@@ -114,3 +114,13 @@ def test_piece_ranges_cover_chunk(built):
         assert pos == cs
     assert f(10, 0, 0, ctypes.byref(b), ctypes.byref(e)) != 0
     assert f(10, 2, 2, ctypes.byref(b), ctypes.byref(e)) != 0
+
+
+def test_time_next_kernel_argument_check(built):
+    """bagua_time_next_kernel needs both events or neither (host-only check)."""
+    lib = ctypes.CDLL(os.path.join(LIB, "libbagua_kernels.so"))
+    f = lib.bagua_time_next_kernel
+    f.restype, f.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
+    assert f(None, None) == 0
+    assert f(ctypes.c_void_p(16), None) == 1
+    assert f(None, ctypes.c_void_p(16)) == 1

@@ -317,3 +317,30 @@ def test_maximum_size_bucket_parity(bc, oracle_c):
     del xh
     oracle_c.decompress_minmax_u8(want, p, dw, F32)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), dw.view(np.uint32))
+
+
+def test_time_next_kernel_records_one_launch(bc):
+    """The measurement hook: the next launch records its own start/stop events; one-shot."""
+    K, N = bc._native.K, bc._native
+    n = 1 << 24
+    x = torch.randn(n, device="cuda")
+    S = K.bagua_minmax_u8_compressed_bytes(F32, n, 1)
+    out = torch.empty(S, dtype=torch.uint8, device="cuda")
+    wsb = K.bagua_minmax_u8_workspace_bytes(n, 1)
+    ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    b.record(st)
+    torch.cuda.synchronize()
+    N.check(K.bagua_time_next_kernel(a.cuda_event, b.cuda_event), "hook")
+    N.check(K.bagua_minmax_u8_compress_stage(1, F32, x.data_ptr(), n, n, 1, out.data_ptr(), S, ws.data_ptr(), wsb, -1,
+                                             ctypes.c_void_p(st.cuda_stream)), "partials")
+    torch.cuda.synchronize()
+    t1 = a.elapsed_time(b)
+    assert 0.0 < t1 < 50.0  # ms: one 64 MiB read
+    # disarmed: a second launch leaves the events alone
+    N.check(K.bagua_minmax_u8_compress_stage(2, F32, x.data_ptr(), n, n, 1, out.data_ptr(), S, ws.data_ptr(), wsb, -1,
+                                             ctypes.c_void_p(st.cuda_stream)), "quantise")
+    torch.cuda.synchronize()
+    assert a.elapsed_time(b) == t1
