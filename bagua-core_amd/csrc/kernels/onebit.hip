@@ -1,12 +1,14 @@
 // onebit.hip — 1-bit sign + scale gradient codec for gfx950 (extension; the
 // reference has only MinMaxUInt8).  Format: DESIGN.md §4.
 //
-// The bit layout is wave-native: one wave owns a 1024-element tile; element
-// r = sub*256 + lane*4 + e of the tile is bit `lane` of u64 word (sub*4+e),
-// so encoding a tile is 16 __ballot()s (v_cmp straight into an SGPR pair)
-// and decoding is 32 v_readlane + a shift per element — no LDS, no
-// cross-lane packing.  Loads/stores stay 16-B (f32) / 8-B (16-bit) per lane,
-// fully coalesced.
+// The bit layout is lane-native: one wave owns a 1024-element tile; element
+// r = sub*256 + lane*4 + e of the tile is bit (sub*4+e) of the 16-bit field at
+// byte 2*lane, i.e. each lane's 16 elements are one field it builds and reads
+// alone (encode: compares + shifts, one shuffle to pair fields into dwords;
+// decode: one 2-byte load and a sign-bit flip per element).  An earlier
+// ballot layout (bit `lane` of word sub*4+e) cost 32 v_readlane per tile to
+// decode.  Element loads/stores are 16 B (f32) / 8 B (16-bit) per lane, and a
+// tile's 128 bit bytes are one coalesced wave access.
 //
 // scale = mean(|x|) with a FIXED summation tree (lane-local pairs, then a
 // 64-lane xor butterfly per tile, then the same 1024-tree over the tile
@@ -143,16 +145,15 @@ __global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
         for (int u = 0; u < TPI; ++u) {
             const int64_t t = t0 + u;
             if (t >= tiles_per_chunk) break;
-            uint32_t word = 0;  // lane l < 32 stores dword l of the 128-byte tile
+            // the lane's 16 sign bits form its own 16-bit field (bit sub*4+e)
+            uint32_t field = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const uint64_t m = __ballot(a[u][k][e] < 0.0f);
-                    const int w = k * 4 + e;
-                    if ((lane >> 1) == w) word = (lane & 1) ? (uint32_t)(m >> 32) : (uint32_t)m;
-                }
-            if (lane < 32) reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane] = word;
+                for (int e = 0; e < 4; ++e) field |= (a[u][k][e] < 0.0f ? 1u : 0u) << (k * 4 + e);
+            // even lanes store their field and the odd neighbour's as one dword
+            const uint32_t next = (uint32_t)__shfl_down((int)field, 1, kWave);
+            if ((lane & 1) == 0) reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane >> 1] = field | (next << 16);
             float ab[4][4];
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -278,20 +279,16 @@ __global__ __launch_bounds__(kBlock) void onebit_decode_kernel(const uint8_t* __
     const int64_t tiles = (cs + kObTile - 1) / kObTile;
     const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
-    // (scalar loads of the tile words were tried: 2.4x slower, s_load latency serialises each wave)
+    const uint32_t sbits = __float_as_uint(scale);
     for (int64_t t = wave; t < tiles; t += nwaves) {
-        const uint32_t mine = lane < 32 ? reinterpret_cast<const uint32_t*>(bits + t * kObTileBytes)[lane] : 0u;
+        // the lane's own 16-bit field: no cross-lane traffic
+        const uint32_t field = reinterpret_cast<const uint16_t*>(bits + t * kObTileBytes)[lane];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             float f[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int w = k * 4 + e;
-                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2 * w);
-                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2 * w + 1);
-                const uint32_t word = lane < 32 ? lo : hi;
-                f[e] = ((word >> (lane & 31)) & 1u) ? -scale : scale;
-            }
+            for (int e = 0; e < 4; ++e)  // bit ? -scale : +scale, as a sign-bit flip
+                f[e] = __uint_as_float(sbits ^ ((field << (31 - (k * 4 + e))) & 0x80000000u));
             store4<T>(dst, t * kObTile + k * 256 + lane * 4, cs, vec, f);
         }
     }

@@ -359,7 +359,8 @@ void orc_addmul_inplace(void* x, const void* y, int dtype, int64_t n, float fact
  * Segment per chunk: 32-byte header {f32 scale, u32 n_valid, 24 zero bytes}
  * followed by ceil(chunk_size/1024) bit tiles of 128 bytes.  Element j of a
  * chunk lives in tile t = j/1024 at r = j%1024 = sub*256 + lane*4 + e; its
- * bit is bit `lane` of little-endian u64 word (sub*4 + e) of the tile.
+ * bit is bit (sub*4 + e) of the little-endian u16 at byte 2*lane of the tile
+ * (each lane's 16 elements form one 16-bit field).
  * bit = (x < 0).  scale = tree_sum(|x|) / n_valid (0 when n_valid == 0).
  * Decode: bit ? -scale : +scale, rounded to T.
  */
@@ -442,19 +443,20 @@ int orc_compress_onebit(const void* in, int dtype, int in_num_elem, int chunk_si
 #pragma omp parallel for schedule(static)
 #endif
         for (int64_t t = 0; t < tiles; ++t) {
-            uint64_t w[16];
+            uint16_t w[64];
             memset(w, 0, sizeof(w));
             for (int r = 0; r < OB_TILE; ++r) {
                 int64_t j = t * OB_TILE + r;
                 if (j >= n_c) break;
                 if (load_f(src, dtype, j) < 0.0f) {
                     int sub = r / 256, lane = (r / 4) % 64, e = r % 4;
-                    w[sub * 4 + e] |= 1ull << lane;
+                    w[lane] |= (uint16_t)(1u << (sub * 4 + e));
                 }
             }
-            for (int k = 0; k < 16; ++k) /* little-endian u64 words */
-                for (int b = 0; b < 8; ++b)
-                    bits[t * OB_TILE_BYTES + k * 8 + b] = (uint8_t)(w[k] >> (8 * b));
+            for (int lane = 0; lane < 64; ++lane) { /* little-endian u16 fields */
+                bits[t * OB_TILE_BYTES + 2 * lane] = (uint8_t)(w[lane] & 0xff);
+                bits[t * OB_TILE_BYTES + 2 * lane + 1] = (uint8_t)(w[lane] >> 8);
+            }
         }
         memset(seg + 32 + (size_t)tiles * OB_TILE_BYTES, 0,
                chunk_offset - 32 - (size_t)tiles * OB_TILE_BYTES);
@@ -485,8 +487,8 @@ int orc_decompress_onebit(const uint8_t* in, size_t in_bytes, int chunk_size, in
             int64_t t = j / OB_TILE;
             int r = (int)(j % OB_TILE);
             int sub = r / 256, lane = (r / 4) % 64, e = r % 4;
-            int byte = (sub * 4 + e) * 8 + lane / 8;
-            int bit = (bits[t * OB_TILE_BYTES + byte] >> (lane % 8)) & 1;
+            int k = sub * 4 + e;
+            int bit = (bits[t * OB_TILE_BYTES + 2 * lane + k / 8] >> (k % 8)) & 1;
             store_f(dst, dtype, j, bit ? -scale : scale);
         }
     }

@@ -269,9 +269,9 @@ def compress_onebit(x: np.ndarray, dtype: int, n_chunks: int, target_chunk: int 
         out[base:base + 32] = head
         neg = np.zeros(tiles * OB_TILE, np.uint8)
         neg[:cs] = seg < 0
-        # [tile][sub][lane][e] -> words [tile][sub*4+e] with bit = lane
-        b = neg.reshape(tiles, 4, 64, 4).transpose(0, 1, 3, 2).reshape(tiles, 16, 64)
-        packed = np.packbits(b, axis=-1, bitorder="little")  # [tile][16][8] bytes
+        # [tile][sub][lane][e] -> per lane a 16-bit field [tile][lane][sub*4+e]
+        b = neg.reshape(tiles, 4, 64, 4).transpose(0, 2, 1, 3).reshape(tiles, 64, 16)
+        packed = np.packbits(b, axis=-1, bitorder="little")  # [tile][64][2] bytes
         out[base + 32:base + 32 + tiles * OB_TILE_BYTES] = packed.reshape(-1)
         out[base + 32 + tiles * OB_TILE_BYTES:base + co] = 0
     if target_chunk == -1:
@@ -286,9 +286,9 @@ def decompress_onebit(buf: np.ndarray, n_chunks: int, out: np.ndarray, dtype: in
     for c in range(n_chunks):
         base = c * co
         scale = np.frombuffer(buf[base:base + 4].tobytes(), np.float32)[0]
-        packed = buf[base + 32:base + 32 + tiles * OB_TILE_BYTES].reshape(tiles, 16, 8)
-        b = np.unpackbits(packed, axis=-1, bitorder="little")  # [tile][16][64]
-        b = b.reshape(tiles, 4, 4, 64).transpose(0, 1, 3, 2).reshape(-1)[:cs]
+        packed = buf[base + 32:base + 32 + tiles * OB_TILE_BYTES].reshape(tiles, 64, 2)
+        b = np.unpackbits(packed, axis=-1, bitorder="little")  # [tile][lane][sub*4+e]
+        b = b.reshape(tiles, 64, 4, 4).transpose(0, 2, 1, 3).reshape(-1)[:cs]
         vals = np.where(b.astype(bool), -scale, scale).astype(np.float32)
         out[c * cs:(c + 1) * cs] = from_f32(vals, dtype)
     return out
