@@ -123,6 +123,18 @@ __device__ __forceinline__ float dequant(uint32_t b, const QParams& q) {
     return ((float)b + q.lower_bound) / q.scale;
 }
 
+// ---------------------------------------------- chunk summation order --
+// block_y_reduce (K:171-194): partial sums s[y] = 0.0f + c[y] + c[y+BY] + ...
+// are folded s[y] += s[y+h] for h = BY/2 .. 1; BY from the launch table K:504-529.
+template <int BY>
+__device__ __forceinline__ void tree_finish(float (&s)[BY]) {
+#pragma unroll
+    for (int h = BY / 2; h >= 1; h /= 2)
+#pragma unroll
+        for (int y = 0; y < h; ++y) s[y] = s[y] + s[y + h];
+}
+inline int reduce_by(int p) { return p <= 4 ? 2 : p <= 8 ? 4 : p <= 16 ? 8 : p <= 32 ? 16 : 32; }
+
 // ------------------------------------------------------------ vectors ------
 // One 16-byte vector of T: 4 x f32 or 8 x 16-bit.
 template <typename T> struct Vec;

@@ -295,6 +295,83 @@ __global__ __launch_bounds__(kBlock) void onebit_decode_kernel(const uint8_t* __
 }
 
 // ------------------------------------------------------------------------
+// fused middle step of the centralized op (1-bit): decode the p received
+// segments of the own chunk, reduce them in the reference's tree order
+// (decompress_from -> reduce_{mean,sum}_inplace, centralized_low_precision_
+// synchronous.rs:40-52) and re-encode the result (compress(target)) in one
+// pass: the reduced chunk is written once, its bits and |x| tile partials come
+// from registers; onebit_finalize_kernel then writes the header.
+// ------------------------------------------------------------------------
+template <typename T, int BY, bool AVG>
+__global__ __launch_bounds__(kBlock) void onebit_reduce_encode_kernel(
+    const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int p, typename T::storage* __restrict__ chunk,
+    uint8_t* __restrict__ out_seg, float* __restrict__ part) {
+    __shared__ float pos[kMaxFusedChunks], neg[kMaxFusedChunks];
+    if (threadIdx.x < p) {  // segment c decodes to +-scale_c as stored in T
+        float sc;
+        __builtin_memcpy(&sc, in + (int64_t)threadIdx.x * chunk_offset, 4);
+        pos[threadIdx.x] = as_stored<T>(sc);
+        neg[threadIdx.x] = as_stored<T>(-sc);
+    }
+    __syncthreads();
+    using S = typename T::storage;
+    const int lane = lane_id();
+    const int64_t tiles = (cs + kObTile - 1) / kObTile;
+    const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    const bool vec = ((uintptr_t)chunk % (4 * sizeof(S))) == 0;
+    const float pf = (float)p;
+    uint8_t* bits = out_seg + 32;
+    for (int64_t t = wave; t < tiles; t += nwaves) {
+        float s[16][BY];
+#pragma unroll
+        for (int b = 0; b < 16; ++b)
+#pragma unroll
+            for (int y = 0; y < BY; ++y) s[b][y] = 0.0f;
+        for (int r = 0; r * BY < p; ++r) {
+            uint32_t f[BY];
+#pragma unroll
+            for (int y = 0; y < BY; ++y) {  // each lane's 16-bit field of every segment
+                const int c = r * BY + y < p ? r * BY + y : p - 1;
+                f[y] = reinterpret_cast<const uint16_t*>(in + (int64_t)c * chunk_offset + 32 + t * kObTileBytes)[lane];
+            }
+#pragma unroll
+            for (int y = 0; y < BY; ++y) {
+                const int c = r * BY + y;
+                if (c >= p) break;
+#pragma unroll
+                for (int b = 0; b < 16; ++b) s[b][y] = s[b][y] + (((f[y] >> b) & 1u) ? neg[c] : pos[c]);
+            }
+        }
+        float x[4][4];
+        uint32_t field = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int b = k * 4 + e;
+                tree_finish<BY>(s[b]);
+                const int64_t j = t * kObTile + k * 256 + lane * 4 + e;
+                // the reduced value as stored in T; padding past cs stays 0 (as the encoder sees it)
+                const float v = j < cs ? as_stored<T>(AVG ? s[b][0] / pf : s[b][0]) : 0.0f;
+                x[k][e] = v;
+                field |= (v < 0.0f ? 1u : 0u) << b;
+            }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) store4<T>(chunk, t * kObTile + k * 256 + lane * 4, cs, vec, x[k]);
+        const uint32_t next = (uint32_t)__shfl_down((int)field, 1, kWave);
+        if ((lane & 1) == 0) reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane >> 1] = field | (next << 16);
+        float ab[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ab[k][e] = __builtin_fabsf(x[k][e]);
+        const float sum = wave_tree_sum(lane_tree(ab));
+        if (lane == 0) part[t] = sum;
+    }
+}
+
+// ------------------------------------------------------------------------
 // host
 // ------------------------------------------------------------------------
 static int64_t ob_tiles(int64_t cs) { return (cs + kObTile - 1) / kObTile; }
@@ -341,6 +418,51 @@ static int ob_decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p,
     return check_launch();
 }
 
+template <typename T, int BY, bool AVG>
+static void launch_ob_reduce(const uint8_t* in, int64_t co, int64_t cs, int p, typename T::storage* chunk,
+                             uint8_t* seg, float* part, int blocks, hipStream_t s) {
+    launch(onebit_reduce_encode_kernel<T, BY, AVG>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p, chunk, seg,
+           part);
+}
+
+template <typename T>
+static int ob_reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, void* tensor,
+                                     int average, uint8_t* out, size_t out_bytes, int target, void* ws,
+                                     size_t ws_bytes, hipStream_t s) {
+    using S = typename T::storage;
+    if (p <= 0 || p > kMaxFusedChunks || cs < 0 || target < 0 || target >= p || !recv || !tensor || !out)
+        return BAGUA_ERR_UNSUPPORTED;  // caller runs decompress + reduce + compress
+    const int64_t co_in = (int64_t)(recv_bytes / (size_t)p), co = (int64_t)(out_bytes / (size_t)p);
+    const int64_t tiles = ob_tiles(cs);
+    if (co_in < 32 + tiles * kObTileBytes || co < 32 + tiles * kObTileBytes) return BAGUA_ERR_INVALID_ARG;
+    if (((uintptr_t)recv + 32) % 4 || co_in % 4 || ((uintptr_t)out + 32) % 4 || co % 4) return BAGUA_ERR_INVALID_ARG;
+    if (!ws || ws_bytes < (size_t)(tiles > 0 ? tiles : 1) * sizeof(float)) return BAGUA_ERR_WORKSPACE;
+    S* chunk = static_cast<S*>(tensor) + (int64_t)target * cs;
+    float* part = static_cast<float*>(ws);
+    uint8_t* seg = out + (int64_t)target * co;
+    if (tiles > 0) {
+        const int blocks = ob_blocks(tiles, 1);
+        switch (reduce_by(p)) {
+            case 2:
+                if (average) launch_ob_reduce<T, 2, true>(recv, co_in, cs, p, chunk, seg, part, blocks, s);
+                else launch_ob_reduce<T, 2, false>(recv, co_in, cs, p, chunk, seg, part, blocks, s);
+                break;
+            case 4:
+                if (average) launch_ob_reduce<T, 4, true>(recv, co_in, cs, p, chunk, seg, part, blocks, s);
+                else launch_ob_reduce<T, 4, false>(recv, co_in, cs, p, chunk, seg, part, blocks, s);
+                break;
+            default:
+                if (average) launch_ob_reduce<T, 8, true>(recv, co_in, cs, p, chunk, seg, part, blocks, s);
+                else launch_ob_reduce<T, 8, false>(recv, co_in, cs, p, chunk, seg, part, blocks, s);
+                break;
+        }
+    }
+    // header + slack of the own segment (the tensor is fully valid: num_elem = p * cs)
+    launch(onebit_finalize_kernel, dim3(1), dim3(kObFinalizeThreads), 0, s, part, tiles, (int64_t)p * cs,
+           (int64_t)cs, target, out, co, (int64_t)out_bytes, p);
+    return check_launch();
+}
+
 }  // namespace bagua
 
 using namespace bagua;
@@ -381,6 +503,24 @@ int bagua_onebit_decompress(int dtype, const uint8_t* input, size_t input_bytes,
         case BAGUA_DTYPE_F32: return ob_decompress_impl<F32>(input, input_bytes, chunk_size, num_chunks, output, s);
         case BAGUA_DTYPE_F16: return ob_decompress_impl<F16>(input, input_bytes, chunk_size, num_chunks, output, s);
         case BAGUA_DTYPE_BF16: return ob_decompress_impl<BF16>(input, input_bytes, chunk_size, num_chunks, output, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+int bagua_onebit_reduce_requantize(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                                   int num_chunks, void* tensor, int average, uint8_t* output, size_t output_bytes,
+                                   int target_chunk, void* workspace, size_t workspace_bytes, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return ob_reduce_requantize_impl<F32>(input, input_bytes, chunk_size, num_chunks, tensor, average, output,
+                                                  output_bytes, target_chunk, workspace, workspace_bytes, s);
+        case BAGUA_DTYPE_F16:
+            return ob_reduce_requantize_impl<F16>(input, input_bytes, chunk_size, num_chunks, tensor, average, output,
+                                                  output_bytes, target_chunk, workspace, workspace_bytes, s);
+        case BAGUA_DTYPE_BF16:
+            return ob_reduce_requantize_impl<BF16>(input, input_bytes, chunk_size, num_chunks, tensor, average,
+                                                   output, output_bytes, target_chunk, workspace, workspace_bytes, s);
     }
     return BAGUA_ERR_UNSUPPORTED;
 }

@@ -22,13 +22,7 @@
 
 namespace bagua {
 
-template <int BY>
-__device__ __forceinline__ void tree_finish(float (&s)[BY]) {
-#pragma unroll
-    for (int h = BY / 2; h >= 1; h /= 2)
-#pragma unroll
-        for (int y = 0; y < h; ++y) s[y] = s[y] + s[y + h];
-}
+
 
 // ---------------------------------------------------------------- plain ----
 template <typename T, int BY, bool AVG, bool VEC>
@@ -92,7 +86,6 @@ __global__ __launch_bounds__(kBlock) void reduce_chunks_kernel(typename T::stora
     }
 }
 
-static int reduce_by(int p) { return p <= 4 ? 2 : p <= 8 ? 4 : p <= 16 ? 8 : p <= 32 ? 16 : 32; }  // K:504-529
 
 template <typename T, int BY, bool AVG>
 static void launch_reduce(typename T::storage* x, int64_t cs, int p, int target, hipStream_t s) {

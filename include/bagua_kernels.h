@@ -87,6 +87,15 @@ int bagua_onebit_compress(int dtype, const void* input, int input_num_element, i
                           size_t workspace_bytes, int target_chunk, bagua_stream_t stream);
 int bagua_onebit_decompress(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
                             int num_chunks, void* output, bagua_stream_t stream);
+/* Middle step of the centralized op with the 1-bit codec, fused: decode the
+ * num_chunks received segments of `input`, reduce them into chunk
+ * `target_chunk` of `tensor` in the reference's summation order (mean if
+ * `average`), and encode that chunk into segment `target_chunk` of `output`.
+ * Equal to bagua_onebit_decompress + bagua_reduce_chunks + bagua_onebit_compress
+ * (target) on a fully valid tensor.  BAGUA_ERR_UNSUPPORTED for num_chunks > 16. */
+int bagua_onebit_reduce_requantize(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                                   int num_chunks, void* tensor, int average, uint8_t* output, size_t output_bytes,
+                                   int target_chunk, void* workspace, size_t workspace_bytes, bagua_stream_t stream);
 
 /* ======================================================================== */
 /* v2 — chunk reduction and elementwise ops                                  */

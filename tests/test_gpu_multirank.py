@@ -139,26 +139,31 @@ def test_centralized_partially_valid_tensor(bc, oracle_c, p, dtype, short):
         assert np.array_equal(host(ts[r], dtype).view(np.uint8), want[r].view(np.uint8)), f"rank {r}"
 
 
-@pytest.mark.parametrize("p", [2, 4])
-def test_centralized_onebit_multirank(bc, oracle_c, p):
+@pytest.mark.parametrize("p,dtype,cs,unfused", [(2, F32, 4096 * 3, False), (4, F32, 4096 * 3, False),
+                                               (3, F32, 5000, False), (8, BF16, 2500, False), (4, F16, 1024, False),
+                                               (16, F32, 3000, False), (4, F32, 4096 * 3, True),
+                                               (8, BF16, 2500, True)])
+def test_centralized_onebit_multirank(bc, oracle_c, p, dtype, cs, unfused):
+    """1-bit centralized op: fused decode+reduce+re-encode (onebit_reduce_encode_kernel) and the
+    unfused sequence against the oracle simulation, every rank bit-for-bit (ragged cs included)."""
     from bagua_core.communicator import loopback_communicators
-    cs = 4096 * 3
-    rng = np.random.default_rng(p)
-    xs = [(rng.standard_normal(p * cs) * 1e-3).astype(np.float32) for _ in range(p)]
-    want = simulate.centralized_low_precision(oracle_c, xs, F32, True, method="OneBitSignScale")
+    rng = np.random.default_rng(p * 31 + cs + dtype)
+    xs = [NP.from_f32((rng.standard_normal(p * cs) * 1e-3 + 2e-4 * r).astype(np.float32), dtype) for r in range(p)]
+    want = simulate.centralized_low_precision(oracle_c, xs, dtype, True, method="OneBitSignScale")
     comms = loopback_communicators(p, 0)
-    ts = [dev(x, F32) for x in xs]
+    ts = [dev(x, dtype) for x in xs]
     torch.cuda.synchronize()
     N = bc._native
+    fn = (N.C.bagua_centralized_low_precision_synchronous_unfused if unfused
+          else N.C.bagua_centralized_low_precision_synchronous)
 
     def rank(r):
         raw = bc.BaguaTensorPy(ts[r], "g").raw()
-        N.check(N.C.bagua_centralized_low_precision_synchronous(comms[r].handle, ctypes.byref(raw), 1,
-                                                                N.COMPRESSION_ONEBIT), f"rank {r}")
+        N.check(fn(comms[r].handle, ctypes.byref(raw), 1, N.COMPRESSION_ONEBIT), f"rank {r}")
 
     run_ranks(rank, p)
     for r in range(p):
-        assert np.array_equal(host(ts[r], F32).view(np.uint32), want[r].view(np.uint32)), f"rank {r}"
+        assert np.array_equal(host(ts[r], dtype).view(np.uint8), want[r].view(np.uint8)), f"rank {r}"
 
 
 @pytest.mark.parametrize("p,dtype,n,unfused,offset", [(2, F32, 30011, False, 0), (3, F32, 30011, False, 0),
