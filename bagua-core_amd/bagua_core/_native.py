@@ -63,6 +63,8 @@ KERNEL_SIGNATURES = {
     "bagua_minmax_u8_compress": (_i32, [_i32, _vp, _i32, _i32, _i32, _vp, _sz, _vp, _sz, _i32, _vp]),
     "bagua_minmax_u8_decompress": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _vp]),
     "bagua_minmax_u8_compress_stage": (_i32, [_i32, _i32, _vp, _i32, _i32, _i32, _vp, _sz, _vp, _sz, _i32, _vp]),
+    "bagua_minmax_u8_resident_path": (_i32, [_i32, _vp, _i32, _i32, _i32, _vp, _sz, _i32, _vp]),
+    "bagua_minmax_u8_resident_trace": (_i32, [_vp]),
     "bagua_minmax_u8_decompress_reduce": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _vp]),
     "bagua_minmax_u8_reduce_requantize": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _vp, _sz, _i32, _vp, _sz,
                                                  _vp]),

@@ -1,0 +1,665 @@
+// minmax_resident.hip — one-launch MinMax-UInt8 encode that keeps part of
+// every chunk on chip across the chunk-wide min/max exchange.
+//
+// The reference encode (bagua_kernels.cu:533-571) reads each chunk three
+// times (cub Min, cub Max, compress_float_to_uint8, K:268-371 + K:455-479);
+// the two-kernel path in minmax_u8.hip reads it twice.  No payload byte can
+// be emitted before the chunk's min/max is known, so the second read is
+// intrinsic to any encoder that streams the chunk from HBM twice — but not to
+// one that keeps what it read.  This kernel runs ONE workgroup per CU (the
+// grid is the CU count), each owning one contiguous slice of a chunk:
+//
+//   pass 1: stream the slice once (default-policy loads): the first
+//           R vectors per lane stay in VGPRs, the next H per lane are parked
+//           in LDS (up to ~156 KiB per CU), the rest are only folded into the
+//           min/max; publish the workgroup's {min, max} as two 8-byte
+//           {tag, value} granules (the data is the flag: one atomic store
+//           each, no fence, MI355X guide Guideline 16 R2)
+//   exchange: one wave re-reads the chunk's granules until every tag is this
+//           launch's, folds them (order-free keys, codec_common.hpp)
+//   pass 2: quantise the streamed part first, in reverse (the lines pass 1
+//           read last are the ones the 256 MiB Infinity Cache still holds),
+//           then the LDS part, then the VGPR part, and write header / slack.
+//
+// Per-launch state lives in a library-owned slot (one per stream) that is
+// never reset: launch k on a slot draws tickets [kG, (k+1)G) from a monotonic
+// counter, so its tag is k+1 (no memset node, graph-replay safe).
+//
+// Residency: the exchange needs every workgroup of a chunk resident at once.
+// The grid equals the CU count and the kernel admits one workgroup per CU,
+// but another stream's kernels can occupy CUs, so the wait is BOUNDED: a
+// workgroup that times out records the launch's tag in `abort_tag` and exits
+// without quantising.  The fixup kernel launched right behind it does
+// nothing unless that tag is set, and then quantises exactly the slices whose
+// `done` word lacks the tag (every partial is published by then: all
+// workgroups of the encode have finished).  The bytes are the same either way.
+//
+// Bit-identity: the same per-element expressions as minmax_quantize_kernel;
+// the min/max is order-free, so slicing cannot change it.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
+
+#include "codec_common.hpp"
+#include "launch_util.hpp"
+
+namespace bagua {
+
+constexpr int kResMaxGrid = 1024;
+constexpr int kResSlots = 64;
+
+struct ResidentSlot {
+    uint64_t ticket;                 // monotonic ticket counter
+    uint32_t abort_tag;              // tag of a launch in which some workgroup gave up waiting
+    uint32_t pad0[13];
+    uint32_t done[kResMaxGrid];      // tag of the launch in which workgroup g quantised its slice
+    uint64_t gran[2 * kResMaxGrid];  // {tag << 32 | min key}, {tag << 32 | max key} per workgroup
+};
+static_assert(sizeof(ResidentSlot) % 64 == 0, "slot alignment");
+
+struct ResidentArgs {
+    const void* in;
+    int64_t cs;            // chunk size (elements)
+    int target;            // -1: all chunks
+    int nact;              // active chunks
+    int bpc;               // workgroups per active chunk
+    int grid;              // launched workgroups (the CU count; idle ones >= nact * bpc)
+    uint8_t* out;
+    int64_t chunk_offset;  // bytes per segment
+    int64_t out_bytes;
+    int num_chunks;
+    ResidentSlot* slot;
+    uint64_t timeout_ticks;  // wall_clock64 ticks a workgroup waits for its chunk's partials
+    uint64_t* trace;         // measurement hook: 8 wall_clock64 slots per workgroup, or nullptr
+};
+
+__device__ __forceinline__ void trace_stamp(const ResidentArgs& a, int g, int k) {
+    if (a.trace != nullptr && threadIdx.x == 0) a.trace[8 * g + k] = wall_clock64();
+}
+
+__device__ __forceinline__ uint32_t tag_of_ticket(uint64_t ticket, int grid) {
+    return (uint32_t)((ticket / (uint64_t)grid) % 0xffffffffull) + 1u;  // never 0 (the zeroed state)
+}
+
+template <typename T, int BLOCK>
+struct SliceGeom {
+    using S = typename T::storage;
+    int c;               // chunk index in the tensor
+    int cl;              // active-chunk index
+    int b;               // slice index within the chunk
+    const S* src;        // chunk start
+    uint8_t* seg;        // chunk's segment
+    uint8_t* payload;    // seg + 32
+    int64_t j0;          // elements before the vector body (scalar head)
+    int64_t nvec;        // body vectors
+    int64_t v0, v1;      // this slice's vectors [v0, v1)
+    bool last;           // last slice of the chunk: owns head, tail and slack
+
+    __device__ __forceinline__ SliceGeom(const ResidentArgs& a, int g) {
+        constexpr int N = Vec<T>::N;
+        cl = g / a.bpc;
+        b = g - cl * a.bpc;
+        c = a.target < 0 ? cl : a.target;
+        src = static_cast<const S*>(a.in) + (int64_t)c * a.cs;
+        seg = a.out + (int64_t)c * a.chunk_offset;
+        payload = seg + 32;
+        const int al = common_alignment<T>((uintptr_t)src, (uintptr_t)payload);  // host checked >= 0
+        j0 = al < a.cs ? al : a.cs;
+        nvec = (a.cs - j0) / N;
+        const int64_t per = ((nvec + a.bpc - 1) / a.bpc + BLOCK - 1) / BLOCK * BLOCK;
+        v0 = (int64_t)b * per;
+        v0 = v0 < nvec ? v0 : nvec;
+        v1 = v0 + per < nvec ? v0 + per : nvec;
+        last = (b == a.bpc - 1);
+    }
+};
+
+template <typename T>
+__device__ __forceinline__ void fold_vec(const uint4& r, uint32_t& lo, uint32_t& hi) {
+    float f[Vec<T>::N];
+    unpack16<T>(r, f);
+#pragma unroll
+    for (int i = 0; i < Vec<T>::N; ++i) {
+        const int32_t k = f2key(f[i]);
+        lo = min(lo, min_space_key(k));
+        hi = min(hi, max_space_key(k));
+    }
+}
+
+template <int SB, int BLOCK, bool NT = false>
+__device__ __forceinline__ void load_tile(const uint4* __restrict__ v, int64_t base, int t, uint4 (&r)[SB]) {
+#pragma unroll
+    for (int j = 0; j < SB; ++j) r[j] = NT ? nt_load16(&v[base + j * BLOCK + t]) : v[base + j * BLOCK + t];
+}
+
+template <typename T>
+__device__ __forceinline__ void quant_store(const uint4& r, const QParams& q, uint8_t* dst) {
+    float f[Vec<T>::N];
+    unpack16<T>(r, f);
+    uint32_t bts[Vec<T>::N];
+#pragma unroll
+    for (int i = 0; i < Vec<T>::N; ++i) bts[i] = quant(f[i], q);
+    store_bytes<T>(dst, bts);
+}
+
+// header of chunk c (slice 0), slack after the payload and the buffer tail
+// (last slice), scalar head and tail elements (last slice) -- the same bytes
+// minmax_quantize_kernel writes
+template <typename T, int BLOCK>
+__device__ void write_extras(const ResidentArgs& a, const SliceGeom<T, BLOCK>& s, float mn, float mx,
+                             const QParams& q) {
+    using S = typename T::storage;
+    constexpr int N = Vec<T>::N;
+    const int t = (int)threadIdx.x;
+    if (s.b == 0 && t < 32) {
+        const uint32_t bmn = sizeof(S) == 4 ? __float_as_uint(mn) : (uint32_t)T::from_f(mn);
+        const uint32_t bmx = sizeof(S) == 4 ? __float_as_uint(mx) : (uint32_t)T::from_f(mx);
+        uint32_t hb = 0;
+        if (t < (int)sizeof(S)) hb = (bmn >> (8 * t)) & 0xff;
+        else if (t < 2 * (int)sizeof(S)) hb = (bmx >> (8 * (t - (int)sizeof(S)))) & 0xff;
+        s.seg[t] = (uint8_t)hb;
+    }
+    if (!s.last) return;
+    for (int64_t j = 32 + a.cs + t; j < a.chunk_offset; j += BLOCK) s.seg[j] = 0;
+    if (a.target < 0 && s.c == a.num_chunks - 1)
+        for (int64_t j = (int64_t)a.num_chunks * a.chunk_offset + t; j < a.out_bytes; j += BLOCK) a.out[j] = 0;
+    for (int64_t j = t; j < s.j0; j += BLOCK) s.payload[j] = (uint8_t)quant(T::to_f(s.src[j]), q);
+    for (int64_t j = s.j0 + s.nvec * N + t; j < a.cs; j += BLOCK)
+        s.payload[j] = (uint8_t)quant(T::to_f(s.src[j]), q);
+}
+
+// one wave folds the granules of active chunk `cl`; false once `deadline` passes
+__device__ __forceinline__ bool sweep_chunk(const ResidentArgs& a, int cl, uint32_t tag, uint64_t deadline,
+                                            uint32_t& lo, uint32_t& hi, bool bounded) {
+    const int lane = lane_id();
+    const uint64_t* g = a.slot->gran + 2 * (int64_t)cl * a.bpc;
+    const int n = 2 * a.bpc;
+    for (;;) {
+        bool ok = true;
+        uint32_t l = 0xffffffffu, h = 0xffffffffu;
+        for (int i = lane; i < n; i += kWave) {
+            const uint64_t x = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok &= (uint32_t)(x >> 32) == tag;
+            if (i & 1) h = min(h, (uint32_t)x);
+            else l = min(l, (uint32_t)x);
+        }
+        if (__all(ok)) {
+            lo = wave_umin(l);
+            hi = wave_umin(h);
+            return true;
+        }
+        if (bounded && wall_clock64() > deadline) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+template <typename T, int BLOCK, int R, int H, int SB, bool NT>
+__global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(ResidentArgs a) {
+    constexpr int N = Vec<T>::N;
+    constexpr int W = BLOCK / kWave;
+    // dynamic LDS only (guide Guideline 17): [H * BLOCK parked vectors][scratch]
+    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+    uint4* park = smem;
+    uint32_t* scratch = reinterpret_cast<uint32_t*>(smem + H * BLOCK);  // 2*W + 4 words
+    const int t = (int)threadIdx.x;
+    const int g = (int)blockIdx.x;
+
+    if (t == 0) {
+        const uint64_t ticket = __hip_atomic_fetch_add(&a.slot->ticket, (uint64_t)1, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        scratch[2 * W] = tag_of_ticket(ticket, a.grid);
+    }
+    __syncthreads();
+    const uint32_t tag = scratch[2 * W];
+    trace_stamp(a, g, 0);
+    if (g >= a.nact * a.bpc) return;  // idle: the grid is the CU count on every launch of the slot
+
+    const SliceGeom<T, BLOCK> s(a, g);
+    const uint4* __restrict__ v = reinterpret_cast<const uint4*>(s.src + s.j0);
+    const int64_t v0 = s.v0, v1 = s.v1;
+    const int64_t stream0 = v0 + (int64_t)(R + H) * BLOCK;  // first streamed vector
+
+    // ---- pass 1 ------------------------------------------------------------
+    uint32_t lo = min_space(T::init_max());
+    uint32_t hi = max_space(-T::init_max());
+    uint4 held[R > 0 ? R : 1];
+    if (v1 > v0) {
+        const int64_t vl = v1 - 1;  // clamp: a duplicate of a slice element never changes the min/max
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t i = v0 + (int64_t)k * BLOCK + t;
+            held[k] = v[i < vl ? i : vl];
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) fold_vec<T>(held[k], lo, hi);
+#pragma unroll
+        for (int kb = 0; kb < H; kb += SB) {
+            uint4 r[SB];
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                if (kb + j < H) {
+                    const int64_t i = v0 + (int64_t)(R + kb + j) * BLOCK + t;
+                    r[j] = v[i < vl ? i : vl];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                if (kb + j < H) {
+                    fold_vec<T>(r[j], lo, hi);
+                    park[(kb + j) * BLOCK + t] = r[j];
+                }
+            }
+        }
+        // streamed part: full tiles double-buffered (2 x SB loads in flight per
+        // lane: with one wave per SIMD nothing else hides the latency), then the
+        // ragged tail tile
+        const int64_t tile = (int64_t)SB * BLOCK;
+        const int64_t nfull = v1 > stream0 ? (v1 - stream0) / tile : 0;
+        if (nfull > 0) {
+            uint4 ra[SB], rb[SB];
+            load_tile<SB, BLOCK>(v, stream0, t, ra);
+            for (int64_t i = 0; i < nfull; i += 2) {
+                // unconditional (clamped) prefetches keep the wait counts static
+                load_tile<SB, BLOCK>(v, stream0 + (i + 1 < nfull ? i + 1 : nfull - 1) * tile, t, rb);
+#pragma unroll
+                for (int j = 0; j < SB; ++j) fold_vec<T>(ra[j], lo, hi);
+                load_tile<SB, BLOCK>(v, stream0 + (i + 2 < nfull ? i + 2 : nfull - 1) * tile, t, ra);
+                if (i + 1 < nfull) {
+#pragma unroll
+                    for (int j = 0; j < SB; ++j) fold_vec<T>(rb[j], lo, hi);
+                }
+            }
+        }
+        for (int j = 0; j < SB; ++j) {
+            const int64_t i = stream0 + nfull * tile + j * BLOCK + t;
+            if (i < v1) fold_vec<T>(v[i], lo, hi);
+        }
+    }
+    if (s.last) {
+        for (int64_t j = t; j < s.j0; j += BLOCK) {
+            const int32_t k = f2key(T::to_f(s.src[j]));
+            lo = min(lo, min_space_key(k));
+            hi = min(hi, max_space_key(k));
+        }
+        for (int64_t j = s.j0 + s.nvec * N + t; j < a.cs; j += BLOCK) {
+            const int32_t k = f2key(T::to_f(s.src[j]));
+            lo = min(lo, min_space_key(k));
+            hi = min(hi, max_space_key(k));
+        }
+    }
+    lo = wave_umin(lo);
+    hi = wave_umin(hi);
+    const int w = t / kWave;
+    if (lane_id() == 0) { scratch[w] = lo; scratch[W + w] = hi; }
+    __syncthreads();
+    if (t == 0) {
+#pragma unroll
+        for (int i = 1; i < W; ++i) { lo = min(lo, scratch[i]); hi = min(hi, scratch[W + i]); }
+        uint64_t* mine = a.slot->gran + 2 * (int64_t)g;
+        __hip_atomic_store(mine, ((uint64_t)tag << 32) | lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(mine + 1, ((uint64_t)tag << 32) | hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+    trace_stamp(a, g, 1);
+    // ---- exchange ------------------------------------------------------------
+    if (w == 0) {
+        const uint64_t deadline = wall_clock64() + a.timeout_ticks;
+        uint32_t l = 0, h = 0;
+        const bool ok = sweep_chunk(a, s.cl, tag, deadline, l, h, true);
+        if (lane_id() == 0) {
+            scratch[2 * W + 1] = ok ? 1u : 0u;
+            scratch[2 * W + 2] = l;
+            scratch[2 * W + 3] = h;
+            if (!ok) __hip_atomic_store(&a.slot->abort_tag, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    if (scratch[2 * W + 1] == 0u) return;  // gave up: the fixup kernel quantises this slice
+    const float mn = from_min_space(scratch[2 * W + 2]), mx = from_max_space(scratch[2 * W + 3]);
+    const QParams q = make_qparams(mn, mx);
+    if (t == 0) a.slot->done[g] = tag;
+    trace_stamp(a, g, 2);
+
+    // ---- pass 2 ------------------------------------------------------------
+    write_extras<T, BLOCK>(a, s, mn, mx, q);
+    uint8_t* vdst = s.payload + s.j0;
+    if (v1 > stream0) {
+        // reverse order (what pass 1 read last is re-read first): the ragged
+        // top tile, then the full tiles double-buffered from the top down
+        const int64_t tile = (int64_t)SB * BLOCK;
+        const int64_t nfull = (v1 - stream0) / tile;
+        for (int j = 0; j < SB; ++j) {
+            const int64_t i = stream0 + nfull * tile + j * BLOCK + t;
+            if (i < v1) quant_store<T>(v[i], q, vdst + i * N);
+        }
+        if (nfull > 0) {
+            uint4 ra[SB], rb[SB];
+            load_tile<SB, BLOCK, NT>(v, stream0 + (nfull - 1) * tile, t, ra);
+            for (int64_t i = nfull - 1; i >= 0; i -= 2) {
+                load_tile<SB, BLOCK, NT>(v, stream0 + (i >= 1 ? i - 1 : 0) * tile, t, rb);
+                const int64_t ba = stream0 + i * tile;
+#pragma unroll
+                for (int j = 0; j < SB; ++j) quant_store<T>(ra[j], q, vdst + (ba + j * BLOCK + t) * N);
+                load_tile<SB, BLOCK, NT>(v, stream0 + (i >= 2 ? i - 2 : 0) * tile, t, ra);
+                if (i >= 1) {
+                    const int64_t bb = ba - tile;
+#pragma unroll
+                    for (int j = 0; j < SB; ++j) quant_store<T>(rb[j], q, vdst + (bb + j * BLOCK + t) * N);
+                }
+            }
+        }
+    }
+    trace_stamp(a, g, 4);
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+        const int64_t i = v0 + (int64_t)(R + k) * BLOCK + t;
+        if (i < v1) quant_store<T>(park[k * BLOCK + t], q, vdst + i * N);
+    }
+    trace_stamp(a, g, 5);
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int64_t i = v0 + (int64_t)k * BLOCK + t;
+        if (i < v1) quant_store<T>(held[k], q, vdst + i * N);
+    }
+    if (a.trace != nullptr) {
+        __syncthreads();
+        trace_stamp(a, g, 3);
+    }
+}
+
+// Runs behind every resident encode on the same stream.  Normal case: one
+// load of abort_tag per workgroup.  After a give-up: quantises every slice
+// whose workgroup did not.
+template <typename T, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void minmax_resident_fixup_kernel(ResidentArgs a) {
+    constexpr int N = Vec<T>::N;
+    __shared__ uint32_t sh[4];
+    const int t = (int)threadIdx.x;
+    const int g = (int)blockIdx.x;
+    if (t == 0) {
+        // the encode took tickets [kG, (k+1)G): the counter now reads (k+1)G
+        const uint64_t ticket = __hip_atomic_load(&a.slot->ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t tag = tag_of_ticket(ticket - 1, a.grid);
+        const uint32_t ab = __hip_atomic_load(&a.slot->abort_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh[0] = tag;
+        sh[1] = (ab == tag && g < a.nact * a.bpc && a.slot->done[g] != tag) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (sh[1] == 0u) return;
+    const uint32_t tag = sh[0];
+    const SliceGeom<T, BLOCK> s(a, g);
+    if (t < kWave) {
+        uint32_t l = 0, h = 0;
+        sweep_chunk(a, s.cl, tag, 0, l, h, false);  // every partial is published: the encode has ended
+        if (t == 0) { sh[2] = l; sh[3] = h; }
+    }
+    __syncthreads();
+    const float mn = from_min_space(sh[2]), mx = from_max_space(sh[3]);
+    const QParams q = make_qparams(mn, mx);
+    write_extras<T, BLOCK>(a, s, mn, mx, q);
+    const uint4* __restrict__ v = reinterpret_cast<const uint4*>(s.src + s.j0);
+    uint8_t* vdst = s.payload + s.j0;
+    for (int64_t i = s.v0 + t; i < s.v1; i += BLOCK) quant_store<T>(v[i], q, vdst + i * N);
+    if (t == 0) a.slot->done[g] = tag;
+}
+
+// ------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------
+struct ResidentDevice {
+    bool init = false, ok = false;
+    int grid = 0;
+    int clock_khz = 0;
+    ResidentSlot* slots = nullptr;
+    int next_slot = 0;
+    std::map<hipStream_t, int> stream_slot;
+};
+static std::mutex g_res_mu;
+static uint64_t* g_res_trace = nullptr;  // bagua_minmax_u8_resident_trace
+static ResidentDevice g_res_dev[64];
+
+// kernel configurations: {BLOCK, R vectors per lane in VGPRs, H per lane in LDS, SB stream batch}
+struct ResidentCfg {
+    int block, r, h, sb;
+    bool nt;  // pass-2 re-reads non-temporal
+};
+static constexpr ResidentCfg kResCfg[] = {
+    {256, 32, 39, 8, false},   // 0
+    {256, 48, 39, 8, false},   // 1
+    {512, 24, 19, 8, false},   // 2
+    {256, 0, 0, 8, false},     // 3: no retention (Infinity Cache only)
+    {256, 32, 0, 8, false},    // 4: VGPRs only
+    {256, 16, 39, 16, false},  // 5
+    {256, 64, 39, 8, false},   // 6
+    {256, 80, 39, 8, false},   // 7
+    {256, 72, 39, 8, false},   // 8
+    {512, 28, 19, 8, false},   // 9
+    {256, 80, 39, 8, true},    // 10
+    {512, 28, 19, 8, true},    // 11
+};
+constexpr int kResNumCfg = (int)(sizeof(kResCfg) / sizeof(kResCfg[0]));
+constexpr int kResDefaultCfg = 11;  // fastest config-2 step (tools/resident_sweep.sh)
+
+static size_t resident_lds_bytes(const ResidentCfg& c) {
+    return (size_t)c.h * c.block * 16 + 16 * ((2 * (c.block / kWave) + 4 + 3) / 4);
+}
+
+template <typename T, int CFG>
+static void* resident_kernel_ptr() {
+    constexpr ResidentCfg c = kResCfg[CFG];
+    return reinterpret_cast<void*>(&minmax_resident_encode_kernel<T, c.block, c.r, c.h, c.sb, c.nt>);
+}
+
+template <typename T>
+static void* resident_kernel_for(int cfg) {
+    switch (cfg) {
+        case 0: return resident_kernel_ptr<T, 0>();
+        case 1: return resident_kernel_ptr<T, 1>();
+        case 2: return resident_kernel_ptr<T, 2>();
+        case 3: return resident_kernel_ptr<T, 3>();
+        case 4: return resident_kernel_ptr<T, 4>();
+        case 5: return resident_kernel_ptr<T, 5>();
+        case 6: return resident_kernel_ptr<T, 6>();
+        case 7: return resident_kernel_ptr<T, 7>();
+        case 8: return resident_kernel_ptr<T, 8>();
+        case 9: return resident_kernel_ptr<T, 9>();
+        case 10: return resident_kernel_ptr<T, 10>();
+        case 11: return resident_kernel_ptr<T, 11>();
+    }
+    return nullptr;
+}
+
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return (e && *e) ? atoi(e) : dflt;
+}
+
+// slot of (device, stream), or nullptr when the resident path is unavailable
+static ResidentSlot* acquire_slot(int dev, hipStream_t s, int* grid, int* clock_khz) {
+    if (dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    ResidentDevice& d = g_res_dev[dev];
+    if (!d.init) {
+        d.init = true;
+        int cus = 0, khz = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return nullptr;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return nullptr;
+        if (cus < 1 || cus > kResMaxGrid || khz < 1) return nullptr;
+        void* p = nullptr;
+        const size_t bytes = sizeof(ResidentSlot) * kResSlots;
+        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            (void)hipFree(p);
+            return nullptr;
+        }
+        d.slots = static_cast<ResidentSlot*>(p);
+        d.grid = cus;
+        d.clock_khz = khz;
+        d.ok = true;
+    }
+    if (!d.ok) return nullptr;
+    auto it = d.stream_slot.find(s);
+    int idx;
+    if (it != d.stream_slot.end()) {
+        idx = it->second;
+    } else {
+        if (d.next_slot >= kResSlots) return nullptr;
+        idx = d.next_slot++;
+        d.stream_slot.emplace(s, idx);
+    }
+    *grid = d.grid;
+    *clock_khz = d.clock_khz;
+    return d.slots + idx;
+}
+
+// Launch plan of the one-launch encode; ok == false: not eligible (the caller
+// runs the two-kernel encode)
+struct ResidentPlan {
+    bool ok = false;
+    int cfg = 0;
+    size_t lds = 0;
+    ResidentArgs a{};
+};
+
+template <typename T>
+static ResidentPlan resident_plan(const void* input, int64_t in_num_elem, int64_t cs, int p, uint8_t* out,
+                                  int64_t out_bytes, int target, hipStream_t s) {
+    using S = typename T::storage;
+    ResidentPlan pl;
+    const int cfg = env_int("BAGUA_RESIDENT_CFG", kResDefaultCfg);
+    if (env_int("BAGUA_RESIDENT", 1) == 0 || cfg < 0 || cfg >= kResNumCfg || p <= 0) return pl;
+    const int nact = target < 0 ? p : 1;
+    const int64_t chunk_offset = out_bytes / p;
+    // whole chunks only, every active chunk fully valid, large enough to pay for the exchange
+    if (in_num_elem < (target < 0 ? (int64_t)p * cs : ((int64_t)target + 1) * cs)) return pl;
+    if (cs * nact < env_int("BAGUA_RESIDENT_MIN_ELEMS", 1 << 22)) return pl;
+    for (int i = 0; i < nact; ++i) {
+        const int c = target < 0 ? i : target;
+        const uintptr_t src = (uintptr_t)(static_cast<const S*>(input) + (int64_t)c * cs);
+        const uintptr_t pay = (uintptr_t)(out + (int64_t)c * chunk_offset + 32);
+        if (src % sizeof(S) != 0 || common_alignment<T>(src, pay) < 0) return pl;
+    }
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return pl;
+    int grid = 0, khz = 0;
+    ResidentSlot* slot = acquire_slot(dev, s, &grid, &khz);
+    if (!slot || nact > grid) return pl;
+    const ResidentCfg& c = kResCfg[cfg];
+    void* kern = resident_kernel_for<T>(cfg);
+    const size_t lds = resident_lds_bytes(c);
+    {
+        // once per (device, dtype, configuration): dynamic LDS above the default, and
+        // one workgroup per CU must be admissible (the exchange needs the grid resident)
+        static int admitted[64][kResNumCfg];  // 0 unknown, 1 yes, -1 no
+        std::lock_guard<std::mutex> lk(g_res_mu);
+        int& st = admitted[dev][cfg];
+        if (st == 0) {
+            int per_cu = 0;
+            st = (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
+                  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, c.block, lds) == hipSuccess &&
+                  per_cu >= 1)
+                     ? 1
+                     : -1;
+            (void)hipGetLastError();
+        }
+        if (st < 0) return pl;
+    }
+    ResidentArgs& a = pl.a;
+    a.in = input;
+    a.cs = cs;
+    a.target = target;
+    a.nact = nact;
+    a.bpc = grid / nact;
+    a.grid = grid;
+    a.out = out;
+    a.chunk_offset = chunk_offset;
+    a.out_bytes = out_bytes;
+    a.num_chunks = p;
+    a.slot = slot;
+    const int64_t us = env_int("BAGUA_RESIDENT_TIMEOUT_US", 20000);
+    a.timeout_ticks = (uint64_t)(us < 0 ? 0 : us) * (uint64_t)khz / 1000u;
+    a.trace = g_res_trace;
+    pl.cfg = cfg;
+    pl.lds = lds;
+    pl.ok = true;
+    return pl;
+}
+
+// BAGUA_ERR_UNSUPPORTED: not eligible (the caller runs the two-kernel encode)
+template <typename T>
+int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, int p, uint8_t* out,
+                           int64_t out_bytes, int target, hipStream_t s) {
+    const ResidentPlan pl = resident_plan<T>(input, in_num_elem, cs, p, out, out_bytes, target, s);
+    if (!pl.ok) return BAGUA_ERR_UNSUPPORTED;
+    const ResidentArgs& a = pl.a;
+    switch (pl.cfg) {
+#define BAGUA_RES_LAUNCH(I)                                                                                 \
+    case I: {                                                                                               \
+        constexpr ResidentCfg k = kResCfg[I];                                                               \
+        launch(minmax_resident_encode_kernel<T, k.block, k.r, k.h, k.sb, k.nt>, dim3(a.grid), dim3(k.block),      \
+               (uint32_t)pl.lds, s, a);                                                                     \
+        launch(minmax_resident_fixup_kernel<T, k.block>, dim3(a.grid), dim3(k.block), 0u, s, a);            \
+        break;                                                                                              \
+    }
+        BAGUA_RES_LAUNCH(0)
+        BAGUA_RES_LAUNCH(1)
+        BAGUA_RES_LAUNCH(2)
+        BAGUA_RES_LAUNCH(3)
+        BAGUA_RES_LAUNCH(4)
+        BAGUA_RES_LAUNCH(5)
+        BAGUA_RES_LAUNCH(6)
+        BAGUA_RES_LAUNCH(7)
+        BAGUA_RES_LAUNCH(8)
+        BAGUA_RES_LAUNCH(9)
+        BAGUA_RES_LAUNCH(10)
+        BAGUA_RES_LAUNCH(11)
+#undef BAGUA_RES_LAUNCH
+    }
+    return check_launch();
+}
+
+template <typename T>
+int resident_eligible(const void* input, int64_t in_num_elem, int64_t cs, int p, uint8_t* out, int64_t out_bytes,
+                      int target, hipStream_t s) {
+    return resident_plan<T>(input, in_num_elem, cs, p, out, out_bytes, target, s).ok ? 1 : 0;
+}
+
+template int resident_compress_impl<F32>(const void*, int64_t, int64_t, int, uint8_t*, int64_t, int, hipStream_t);
+template int resident_compress_impl<F16>(const void*, int64_t, int64_t, int, uint8_t*, int64_t, int, hipStream_t);
+template int resident_compress_impl<BF16>(const void*, int64_t, int64_t, int, uint8_t*, int64_t, int, hipStream_t);
+
+}  // namespace bagua
+
+extern "C" int bagua_minmax_u8_resident_trace(void* device_buffer) {
+    std::lock_guard<std::mutex> lk(bagua::g_res_mu);
+    bagua::g_res_trace = static_cast<uint64_t*>(device_buffer);
+    return BAGUA_OK;
+}
+
+extern "C" int bagua_minmax_u8_resident_path(int dtype, const void* input, int input_num_element, int chunk_size,
+                                             int num_chunks, uint8_t* output, size_t output_bytes, int target_chunk,
+                                             bagua_stream_t stream) {
+    using namespace bagua;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (num_chunks <= 0 || chunk_size < 0 || target_chunk < -1 || target_chunk >= num_chunks || !input || !output)
+        return 0;
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return resident_eligible<F32>(input, input_num_element, chunk_size, num_chunks, output,
+                                          (int64_t)output_bytes, target_chunk, s);
+        case BAGUA_DTYPE_F16:
+            return resident_eligible<F16>(input, input_num_element, chunk_size, num_chunks, output,
+                                          (int64_t)output_bytes, target_chunk, s);
+        case BAGUA_DTYPE_BF16:
+            return resident_eligible<BF16>(input, input_num_element, chunk_size, num_chunks, output,
+                                           (int64_t)output_bytes, target_chunk, s);
+    }
+    return 0;
+}
+
+namespace bagua {
+
+}  // namespace bagua

@@ -314,6 +314,11 @@ int minmax_partials_blocks(int64_t cs, int per_vec, int nact, size_t ws_bytes) {
     return nblk > cap ? (int)cap : nblk;
 }
 
+// defined in minmax_resident.hip; BAGUA_ERR_UNSUPPORTED when the shape is not eligible
+template <typename T>
+int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, int p, uint8_t* out,
+                           int64_t out_bytes, int target, hipStream_t s);
+
 // stage bit 1: min/max partials pass; bit 2: quantise pass (3 = whole compress).
 // Both stages derive the same partials count from the same arguments.
 template <typename T>
@@ -331,6 +336,10 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
     const int nblk = ws ? minmax_partials_blocks(cs, Vec<T>::N, nact, ws_bytes) : 0;
     if (nblk < 1) return BAGUA_ERR_WORKSPACE;
     uint2* partials = static_cast<uint2*>(ws);
+    if (stages == 3 && e0 == 0 && e1 == cs) {  // one-launch encode when eligible (minmax_resident.hip)
+        const int rc = resident_compress_impl<T>(input, in_num_elem, cs, p, out, (int64_t)out_bytes, target, s);
+        if (rc != BAGUA_ERR_UNSUPPORTED) return rc;
+    }
     if (stages & 1)
         launch(minmax_partials_kernel<T>, dim3(nblk, nact), dim3(kBlock), 0, s,
                            static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, partials);

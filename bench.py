@@ -105,6 +105,21 @@ def bench_codec(args, onebit: bool = False):
             return [lambda: K.bagua_onebit_compress(dcode, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
                     lambda: K.bagua_onebit_decompress(dcode, cp, S, n, p, yp, sp)]
         alg = [esz * n + n // 8 + 4 * ((n + 1023) // 1024), n // 8 + 32 + esz * n]  # + per-tile |x| partials
+    elif K.bagua_minmax_u8_resident_path(dcode, xp, n, n, p, cp, S, -1, sp) == 1:
+        # one-launch encode (minmax_resident.hip): pass 1 keeps part of the bucket in
+        # VGPRs/LDS across the min/max exchange; the compress call also launches the
+        # (normally empty) fixup kernel, which the step's wall clock includes
+        names = ["minmax_resident_encode_kernel", "minmax_dequantize_kernel"]
+
+        def launches():
+            return [lambda: K.bagua_minmax_u8_compress(dcode, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
+                    lambda: K.bagua_minmax_u8_decompress(dcode, cp, S, n, p, yp, sp)]
+        # algorithmic bytes per launch as SURVEY §8(d) counts them: encode 4N (min/max read) +
+        # 4N (quantise read) + N + header, decode N + header read, 4N written.  This kernel
+        # serves part of the second read from VGPRs/LDS; its compulsory bytes (4N + N) are
+        # reported beside it (roofline.compulsory_*).
+        alg = [2 * esz * n + n + 32, n + 32 + esz * n]
+        compulsory = [esz * n + n + 32, n + 32 + esz * n]
     else:
         names = ["minmax_partials_kernel", "minmax_quantize_kernel", "minmax_dequantize_kernel"]
 
@@ -115,6 +130,8 @@ def bench_codec(args, onebit: bool = False):
         # algorithmic bytes per launch: partials read 4N; quantise read 4N + write N + header;
         # dequantise read N + header, write 4N.  Sum = 14N + 64p.
         alg = [esz * n, esz * n + n + 32, n + 32 + esz * n]
+    if "compulsory" not in locals():
+        compulsory = alg
     calls = launches()
 
     def step():
@@ -169,12 +186,15 @@ def bench_codec(args, onebit: bool = False):
     traffic = pmc_traffic(names[dom]) if (args.dtype == "f32" and n == (1 << 26) and not onebit) else None
     roof = {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "alg_bytes_per_launch": alg[dom], "avg_launch_us": round(per[dom] * 1e3, 2)}
+            "alg_bytes_per_launch": alg[dom], "avg_launch_us": round(per[dom] * 1e3, 2),
+            "compulsory_bytes_per_launch": compulsory[dom],
+            "compulsory_frac": round(compulsory[dom] / (per[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     extra = {
         "per_kernel_us": {nm: round(t * 1e3, 2) for nm, t in zip(names, per)},
         "per_kernel_gbs": {nm: round(a / (t * 1e-3) / 1e9, 1) for nm, a, t in zip(names, alg, per)},
         # whole step by wall clock (launch gaps included): 14N + 64p algorithmic bytes
-        "step_roofline": {"alg_bytes": step_alg, "wall_us": round(ms * 1e3, 2),
+        "step_roofline": {"alg_bytes": step_alg, "compulsory_bytes": sum(compulsory),
+                          "wall_us": round(ms * 1e3, 2),
                           "achieved_gbs": round(step_alg / (ms * 1e-3) / 1e9, 1),
                           "frac": round(step_alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "per_kernel_note": "kernel-recorded HIP events (hipExtLaunchKernel); dominant kernel over the timed region, "

@@ -73,6 +73,18 @@ int bagua_minmax_u8_compress_stage(int stage, int dtype, const void* input, int 
                                    int chunk_size, int num_chunks, uint8_t* output, size_t output_bytes,
                                    void* workspace, size_t workspace_bytes, int target_chunk,
                                    bagua_stream_t stream);
+/* 1 when bagua_minmax_u8_compress would take the one-launch encode for these
+ * arguments on this stream (whole, fully valid chunks of >= 4 Mi elements in
+ * total, vector-alignable payloads), 0 when it runs the
+ * two-pass encode.  Measurement and tests only; no launch. */
+int bagua_minmax_u8_resident_path(int dtype, const void* input, int input_num_element, int chunk_size,
+                                  int num_chunks, uint8_t* output, size_t output_bytes, int target_chunk,
+                                  bagua_stream_t stream);
+/* Measurement hook: while set, every one-launch encode writes wall_clock64
+ * stamps into `device_buffer` (>= 8 * CU count u64), 8 slots per workgroup:
+ * start, end of pass 1, exchange done, end of pass 2, end of the streamed
+ * part of pass 2, end of its LDS part.  NULL disarms. */
+int bagua_minmax_u8_resident_trace(void* device_buffer);
 /* decompress_uint8_to_{f32,f16}_host (K:667-681) */
 int bagua_minmax_u8_decompress(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
                                int num_chunks, void* output, bagua_stream_t stream);
