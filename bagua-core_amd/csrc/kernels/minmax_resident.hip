@@ -579,7 +579,11 @@ static ResidentPlan resident_plan(const void* input, int64_t in_num_elem, int64_
     a.out_bytes = out_bytes;
     a.num_chunks = p;
     a.slot = slot;
-    const int64_t us = env_int("BAGUA_RESIDENT_TIMEOUT_US", 20000);
+    // bounded wait: the exchange normally completes a few us after the slowest
+    // workgroup's pass 1, which reads the active chunks; allow that pass to run
+    // at as little as 0.5 TB/s before giving up (then the fixup kernel quantises)
+    const int64_t active_bytes = cs * nact * (int64_t)sizeof(S);
+    const int64_t us = env_int("BAGUA_RESIDENT_TIMEOUT_US", (int)(200 + active_bytes / 500000));
     a.timeout_ticks = (uint64_t)(us < 0 ? 0 : us) * (uint64_t)khz / 1000u;
     a.trace = g_res_trace;
     pl.cfg = cfg;

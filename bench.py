@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--pieces", type=int, default=0,
                     help="pipelined all-reduce pieces per chunk (0 = automatic, 1 = unpieced)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--two-pass", action="store_true",
+                    help="codec workload: force the two-kernel MinMax encode (BAGUA_RESIDENT=0) for A/B")
     ap.add_argument("--no-decentralized", action="store_true", help="skip the config-5 side measurement (N > 1)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the cpu_baseline leg")
     return ap.parse_args()
@@ -476,6 +478,8 @@ def main():
     sys.stdout.flush()
     os.dup2(2, 1)
     args = parse()
+    if args.two_pass:
+        os.environ["BAGUA_RESIDENT"] = "0"  # read by the kernel library on every compress call
     world = int(os.environ.get("WORLD_SIZE", args.gpus))
     rank = int(os.environ.get("RANK", 0))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))

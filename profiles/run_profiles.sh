@@ -20,6 +20,13 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch"
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > /dev/null
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > /dev/null
+# the two-pass encode (BAGUA_RESIDENT=0) for comparison
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_2p" -o twopass -- \
+    python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --two-pass > "$OUT/twopass_under_rocprof.json"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_2p" -o run -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --two-pass > /dev/null
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_2p" -o run -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --two-pass > /dev/null
 # python3 profiles/collect_pmc.py "$OUT/fetch" "$OUT/write" "profiles/${R}_pmc_traffic.json"
 # (run locally on the merged gpurun_out/: only gpurun_out/ returns from the box)
 # cp "$(find "$OUT/trace" -name '*kernel_stats.csv' | head -1)" "profiles/${R}_bench_n1_kernel_stats.csv"
