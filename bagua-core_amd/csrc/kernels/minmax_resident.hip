@@ -28,11 +28,12 @@
 // Residency: the exchange needs every workgroup of a chunk resident at once.
 // The grid equals the CU count and the kernel admits one workgroup per CU,
 // but another stream's kernels can occupy CUs, so the wait is BOUNDED: a
-// workgroup that times out records the launch's tag in `abort_tag` and exits
-// without quantising.  The fixup kernel launched right behind it does
-// nothing unless that tag is set, and then quantises exactly the slices whose
-// `done` word lacks the tag (every partial is published by then: all
-// workgroups of the encode have finished).  The bytes are the same either way.
+// workgroup that times out folds every slice whose partials are still
+// missing straight from memory (min/max is order-free and idempotent, so any
+// mix of published partials and re-read slices is the chunk's exact min/max)
+// and quantises its own slice.  The late workgroup, once it runs, finds the
+// partials of all the others published and finishes normally.  No second
+// kernel, no spin without a deadline; the bytes are the same either way.
 //
 // Bit-identity: the same per-element expressions as minmax_quantize_kernel;
 // the min/max is order-free, so slicing cannot change it.
@@ -53,9 +54,7 @@ constexpr int kResSlots = 64;
 
 struct ResidentSlot {
     uint64_t ticket;                 // monotonic ticket counter
-    uint32_t abort_tag;              // tag of a launch in which some workgroup gave up waiting
-    uint32_t pad0[13];
-    uint32_t done[kResMaxGrid];      // tag of the launch in which workgroup g quantised its slice
+    uint64_t pad0[7];
     uint64_t gran[2 * kResMaxGrid];  // {tag << 32 | min key}, {tag << 32 | max key} per workgroup
 };
 static_assert(sizeof(ResidentSlot) % 64 == 0, "slot alignment");
@@ -129,6 +128,24 @@ __device__ __forceinline__ void fold_vec(const uint4& r, uint32_t& lo, uint32_t&
     }
 }
 
+// the scalar head and tail elements of a chunk (owned by its last slice)
+template <typename T, int BLOCK>
+__device__ __forceinline__ void fold_scalars(const ResidentArgs& a, const SliceGeom<T, BLOCK>& s, uint32_t& lo,
+                                             uint32_t& hi) {
+    constexpr int N = Vec<T>::N;
+    const int t = (int)threadIdx.x;
+    for (int64_t j = t; j < s.j0; j += BLOCK) {
+        const int32_t k = f2key(T::to_f(s.src[j]));
+        lo = min(lo, min_space_key(k));
+        hi = min(hi, max_space_key(k));
+    }
+    for (int64_t j = s.j0 + s.nvec * N + t; j < a.cs; j += BLOCK) {
+        const int32_t k = f2key(T::to_f(s.src[j]));
+        lo = min(lo, min_space_key(k));
+        hi = min(hi, max_space_key(k));
+    }
+}
+
 template <int SB, int BLOCK, bool NT = false>
 __device__ __forceinline__ void load_tile(const uint4* __restrict__ v, int64_t base, int t, uint4 (&r)[SB]) {
 #pragma unroll
@@ -193,6 +210,31 @@ __device__ __forceinline__ bool sweep_chunk(const ResidentArgs& a, int cl, uint3
         }
         if (bounded && wall_clock64() > deadline) return false;
         __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// after a give-up: the calling thread's share of the chunk's min/max, taking a
+// slice's published partials when both carry this launch's tag and re-reading
+// the slice otherwise.  Threads may disagree about a granule that lands
+// meanwhile; every slice is then still covered whole (by the granule some
+// thread took, or by all threads' strided re-reads), so the union is exact.
+template <typename T, int BLOCK>
+__device__ void fold_missing_slices(const ResidentArgs& a, int cl, uint32_t tag, uint32_t& lo, uint32_t& hi) {
+    const int t = (int)threadIdx.x;
+    for (int b = 0; b < a.bpc; ++b) {
+        const int gg = cl * a.bpc + b;
+        const uint64_t* gr = a.slot->gran + 2 * (int64_t)gg;
+        const uint64_t x0 = __hip_atomic_load(gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t x1 = __hip_atomic_load(gr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(x0 >> 32) == tag && (uint32_t)(x1 >> 32) == tag) {
+            lo = min(lo, (uint32_t)x0);
+            hi = min(hi, (uint32_t)x1);
+            continue;
+        }
+        const SliceGeom<T, BLOCK> sg(a, gg);
+        const uint4* __restrict__ v = reinterpret_cast<const uint4*>(sg.src + sg.j0);
+        for (int64_t i = sg.v0 + t; i < sg.v1; i += BLOCK) fold_vec<T>(v[i], lo, hi);
+        if (sg.last) fold_scalars<T, BLOCK>(a, sg, lo, hi);
     }
 }
 
@@ -278,18 +320,7 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
             if (i < v1) fold_vec<T>(v[i], lo, hi);
         }
     }
-    if (s.last) {
-        for (int64_t j = t; j < s.j0; j += BLOCK) {
-            const int32_t k = f2key(T::to_f(s.src[j]));
-            lo = min(lo, min_space_key(k));
-            hi = min(hi, max_space_key(k));
-        }
-        for (int64_t j = s.j0 + s.nvec * N + t; j < a.cs; j += BLOCK) {
-            const int32_t k = f2key(T::to_f(s.src[j]));
-            lo = min(lo, min_space_key(k));
-            hi = min(hi, max_space_key(k));
-        }
-    }
+    if (s.last) fold_scalars<T, BLOCK>(a, s, lo, hi);
     lo = wave_umin(lo);
     hi = wave_umin(hi);
     const int w = t / kWave;
@@ -313,14 +344,27 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
             scratch[2 * W + 1] = ok ? 1u : 0u;
             scratch[2 * W + 2] = l;
             scratch[2 * W + 3] = h;
-            if (!ok) __hip_atomic_store(&a.slot->abort_tag, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
-    if (scratch[2 * W + 1] == 0u) return;  // gave up: the fixup kernel quantises this slice
+    if (scratch[2 * W + 1] == 0u) {
+        // gave up waiting: the whole workgroup folds the missing slices itself
+        uint32_t l = 0xffffffffu, h = 0xffffffffu;
+        fold_missing_slices<T, BLOCK>(a, s.cl, tag, l, h);
+        l = wave_umin(l);
+        h = wave_umin(h);
+        if (lane_id() == 0) { scratch[w] = l; scratch[W + w] = h; }
+        __syncthreads();
+        if (t == 0) {
+#pragma unroll
+            for (int i = 1; i < W; ++i) { l = min(l, scratch[i]); h = min(h, scratch[W + i]); }
+            scratch[2 * W + 2] = l;
+            scratch[2 * W + 3] = h;
+        }
+        __syncthreads();
+    }
     const float mn = from_min_space(scratch[2 * W + 2]), mx = from_max_space(scratch[2 * W + 3]);
     const QParams q = make_qparams(mn, mx);
-    if (t == 0) a.slot->done[g] = tag;
     trace_stamp(a, g, 2);
 
     // ---- pass 2 ------------------------------------------------------------
@@ -368,42 +412,6 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
         __syncthreads();
         trace_stamp(a, g, 3);
     }
-}
-
-// Runs behind every resident encode on the same stream.  Normal case: one
-// load of abort_tag per workgroup.  After a give-up: quantises every slice
-// whose workgroup did not.
-template <typename T, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void minmax_resident_fixup_kernel(ResidentArgs a) {
-    constexpr int N = Vec<T>::N;
-    __shared__ uint32_t sh[4];
-    const int t = (int)threadIdx.x;
-    const int g = (int)blockIdx.x;
-    if (t == 0) {
-        // the encode took tickets [kG, (k+1)G): the counter now reads (k+1)G
-        const uint64_t ticket = __hip_atomic_load(&a.slot->ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t tag = tag_of_ticket(ticket - 1, a.grid);
-        const uint32_t ab = __hip_atomic_load(&a.slot->abort_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sh[0] = tag;
-        sh[1] = (ab == tag && g < a.nact * a.bpc && a.slot->done[g] != tag) ? 1u : 0u;
-    }
-    __syncthreads();
-    if (sh[1] == 0u) return;
-    const uint32_t tag = sh[0];
-    const SliceGeom<T, BLOCK> s(a, g);
-    if (t < kWave) {
-        uint32_t l = 0, h = 0;
-        sweep_chunk(a, s.cl, tag, 0, l, h, false);  // every partial is published: the encode has ended
-        if (t == 0) { sh[2] = l; sh[3] = h; }
-    }
-    __syncthreads();
-    const float mn = from_min_space(sh[2]), mx = from_max_space(sh[3]);
-    const QParams q = make_qparams(mn, mx);
-    write_extras<T, BLOCK>(a, s, mn, mx, q);
-    const uint4* __restrict__ v = reinterpret_cast<const uint4*>(s.src + s.j0);
-    uint8_t* vdst = s.payload + s.j0;
-    for (int64_t i = s.v0 + t; i < s.v1; i += BLOCK) quant_store<T>(v[i], q, vdst + i * N);
-    if (t == 0) a.slot->done[g] = tag;
 }
 
 // ------------------------------------------------------------------------
@@ -581,7 +589,8 @@ static ResidentPlan resident_plan(const void* input, int64_t in_num_elem, int64_
     a.slot = slot;
     // bounded wait: the exchange normally completes a few us after the slowest
     // workgroup's pass 1, which reads the active chunks; allow that pass to run
-    // at as little as 0.5 TB/s before giving up (then the fixup kernel quantises)
+    // at as little as 0.5 TB/s before giving up (then the waiting workgroups
+    // re-read the missing slices themselves)
     const int64_t active_bytes = cs * nact * (int64_t)sizeof(S);
     const int64_t us = env_int("BAGUA_RESIDENT_TIMEOUT_US", (int)(200 + active_bytes / 500000));
     a.timeout_ticks = (uint64_t)(us < 0 ? 0 : us) * (uint64_t)khz / 1000u;
@@ -605,7 +614,6 @@ int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, i
         constexpr ResidentCfg k = kResCfg[I];                                                               \
         launch(minmax_resident_encode_kernel<T, k.block, k.r, k.h, k.sb, k.nt>, dim3(a.grid), dim3(k.block),      \
                (uint32_t)pl.lds, s, a);                                                                     \
-        launch(minmax_resident_fixup_kernel<T, k.block>, dim3(a.grid), dim3(k.block), 0u, s, a);            \
         break;                                                                                              \
     }
         BAGUA_RES_LAUNCH(0)

@@ -299,10 +299,12 @@ __global__ __launch_bounds__(kBlock) void onebit_decode_kernel(const uint8_t* __
 // segments of the own chunk, reduce them in the reference's tree order
 // (decompress_from -> reduce_{mean,sum}_inplace, centralized_low_precision_
 // synchronous.rs:40-52) and re-encode the result (compress(target)) in one
-// pass: the reduced chunk is written once, its bits and |x| tile partials come
-// from registers; onebit_finalize_kernel then writes the header.
+// pass: the reduced chunk is written once (or not at all when the caller
+// overwrites it anyway, STORE = false: the centralized op's final decompress
+// rewrites every element), its bits and |x| tile partials come from registers;
+// onebit_finalize_kernel then writes the header.
 // ------------------------------------------------------------------------
-template <typename T, int BY, bool AVG>
+template <typename T, int BY, bool AVG, bool STORE>
 __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_kernel(
     const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int p, typename T::storage* __restrict__ chunk,
     uint8_t* __restrict__ out_seg, float* __restrict__ part) {
@@ -357,8 +359,10 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_kernel(
                 x[k][e] = v;
                 field |= (v < 0.0f ? 1u : 0u) << b;
             }
+        if constexpr (STORE) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) store4<T>(chunk, t * kObTile + k * 256 + lane * 4, cs, vec, x[k]);
+            for (int k = 0; k < 4; ++k) store4<T>(chunk, t * kObTile + k * 256 + lane * 4, cs, vec, x[k]);
+        }
         const uint32_t next = (uint32_t)__shfl_down((int)field, 1, kWave);
         if ((lane & 1) == 0) reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane >> 1] = field | (next << 16);
         float ab[4][4];
@@ -421,8 +425,12 @@ static int ob_decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p,
 template <typename T, int BY, bool AVG>
 static void launch_ob_reduce(const uint8_t* in, int64_t co, int64_t cs, int p, typename T::storage* chunk,
                              uint8_t* seg, float* part, int blocks, hipStream_t s) {
-    launch(onebit_reduce_encode_kernel<T, BY, AVG>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p, chunk, seg,
-           part);
+    if (chunk)
+        launch(onebit_reduce_encode_kernel<T, BY, AVG, true>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p, chunk,
+               seg, part);
+    else
+        launch(onebit_reduce_encode_kernel<T, BY, AVG, false>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
+               chunk, seg, part);
 }
 
 template <typename T>
@@ -430,14 +438,14 @@ static int ob_reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int
                                      int average, uint8_t* out, size_t out_bytes, int target, void* ws,
                                      size_t ws_bytes, hipStream_t s) {
     using S = typename T::storage;
-    if (p <= 0 || p > kMaxFusedChunks || cs < 0 || target < 0 || target >= p || !recv || !tensor || !out)
+    if (p <= 0 || p > kMaxFusedChunks || cs < 0 || target < 0 || target >= p || !recv || !out)
         return BAGUA_ERR_UNSUPPORTED;  // caller runs decompress + reduce + compress
     const int64_t co_in = (int64_t)(recv_bytes / (size_t)p), co = (int64_t)(out_bytes / (size_t)p);
     const int64_t tiles = ob_tiles(cs);
     if (co_in < 32 + tiles * kObTileBytes || co < 32 + tiles * kObTileBytes) return BAGUA_ERR_INVALID_ARG;
     if (((uintptr_t)recv + 32) % 4 || co_in % 4 || ((uintptr_t)out + 32) % 4 || co % 4) return BAGUA_ERR_INVALID_ARG;
     if (!ws || ws_bytes < (size_t)(tiles > 0 ? tiles : 1) * sizeof(float)) return BAGUA_ERR_WORKSPACE;
-    S* chunk = static_cast<S*>(tensor) + (int64_t)target * cs;
+    S* chunk = tensor ? static_cast<S*>(tensor) + (int64_t)target * cs : nullptr;  // nullptr: not stored
     float* part = static_cast<float*>(ws);
     uint8_t* seg = out + (int64_t)target * co;
     if (tiles > 0) {

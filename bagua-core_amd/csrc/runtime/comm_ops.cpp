@@ -103,8 +103,9 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
         const size_t ws_bytes = bagua_onebit_workspace_bytes((int)k.cs, 1);
         const uint64_t ws = stream_workspace(c->device_id, s, ws_bytes);
         if (!ws) return finish(c, BAGUA_ERR_OOM);
+        // the reduced chunk is not stored: step 5's decompress rewrites every element
         rc = bagua_onebit_reduce_requantize(t->dtype, recv.as<uint8_t>(), k.S, (int)k.cs, k.p,
-                                            (void*)(uintptr_t)t->ptr, average, send.as<uint8_t>(), k.S, k.rank,
+                                            nullptr, average, send.as<uint8_t>(), k.S, k.rank,
                                             (void*)(uintptr_t)ws, ws_bytes, (void*)(uintptr_t)s);
         if (rc == BAGUA_OK) done = true;
         else if (rc != BAGUA_ERR_UNSUPPORTED) return finish(c, rc);

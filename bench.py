@@ -109,8 +109,7 @@ def bench_codec(args, onebit: bool = False):
         alg = [esz * n + n // 8 + 4 * ((n + 1023) // 1024), n // 8 + 32 + esz * n]  # + per-tile |x| partials
     elif K.bagua_minmax_u8_resident_path(dcode, xp, n, n, p, cp, S, -1, sp) == 1:
         # one-launch encode (minmax_resident.hip): pass 1 keeps part of the bucket in
-        # VGPRs/LDS across the min/max exchange; the compress call also launches the
-        # (normally empty) fixup kernel, which the step's wall clock includes
+        # VGPRs/LDS across the min/max exchange (a single kernel per compress call)
         names = ["minmax_resident_encode_kernel", "minmax_dequantize_kernel"]
 
         def launches():

@@ -104,7 +104,9 @@ int bagua_onebit_decompress(int dtype, const uint8_t* input, size_t input_bytes,
  * `target_chunk` of `tensor` in the reference's summation order (mean if
  * `average`), and encode that chunk into segment `target_chunk` of `output`.
  * Equal to bagua_onebit_decompress + bagua_reduce_chunks + bagua_onebit_compress
- * (target) on a fully valid tensor.  BAGUA_ERR_UNSUPPORTED for num_chunks > 16. */
+ * (target) on a fully valid tensor.  BAGUA_ERR_UNSUPPORTED for num_chunks > 16.
+ * `tensor` may be NULL: the reduced chunk is then only encoded, not stored
+ * (the centralized op overwrites it with its final decompress anyway). */
 int bagua_onebit_reduce_requantize(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
                                    int num_chunks, void* tensor, int average, uint8_t* output, size_t output_bytes,
                                    int target_chunk, void* workspace, size_t workspace_bytes, bagua_stream_t stream);

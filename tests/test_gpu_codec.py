@@ -241,6 +241,42 @@ def test_onebit_goldens(bc, goldens):
         assert_float_bits_equal(to_host(out, dtype), goldens[f"ob_dec_{i}"], dtype, f"onebit decode {i}")
 
 
+@pytest.mark.parametrize("dtype", [F32, F16, BF16])
+@pytest.mark.parametrize("p", [1, 2, 5, 8, 16])
+@pytest.mark.parametrize("store", [True, False])
+def test_onebit_fused_reduce_requantize(bc, oracle_c, dtype, p, store):
+    """bagua_onebit_reduce_requantize == decompress_from + reduce_mean + compress(target); with a
+    NULL tensor the same segment is encoded and nothing of the tensor is written."""
+    from oracle import oracle_np as NP
+    rng = np.random.default_rng(300 + p + dtype)
+    cs = 3 * 1024 + 8 * p + 5  # ragged last tile
+    xs = [NP.from_f32((rng.standard_normal(p * cs) * 1e-3 + 1e-4).astype(np.float32), dtype) for _ in range(p)]
+    r = p - 1
+    comps = [oracle_c.compress_onebit(x, dtype, p) for x in xs]
+    S = comps[0].size
+    co = S // p
+    recv = np.concatenate([c[r * co:(r + 1) * co] for c in comps])
+    t_want = np.zeros(p * cs, STORAGE[dtype])
+    oracle_c.decompress_onebit(recv, p, t_want, dtype)
+    oracle_c.reduce_chunks(t_want, dtype, p, r, True)
+    send_want = np.zeros(S, np.uint8)
+    oracle_c.compress_onebit(t_want, dtype, p, r, out=send_want)
+    K = bc._native.K
+    recv_d = torch.from_numpy(recv).cuda()
+    t_d = torch.full((p * cs,), 7.0, dtype=TORCH[dtype], device="cuda")
+    send_d = torch.zeros(S, dtype=torch.uint8, device="cuda")
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
+    rc = K.bagua_onebit_reduce_requantize(dtype, recv_d.data_ptr(), S, cs, p, t_d.data_ptr() if store else None,
+                                          1, send_d.data_ptr(), S, r, ws.data_ptr(), ws.numel(), None)
+    assert rc == 0
+    got_t = to_host(t_d, dtype)
+    if store:
+        assert_float_bits_equal(got_t[r * cs:(r + 1) * cs], t_want[r * cs:(r + 1) * cs], dtype, "reduced chunk")
+    else:
+        assert np.all(got_t.astype(np.float32) == 7.0) if dtype != BF16 else np.all(got_t == 0x40E0)
+    assert np.array_equal(segment_bytes(send_d.cpu().numpy(), p, r), segment_bytes(send_want, p, r))
+
+
 @pytest.mark.parametrize("dtype", [F32, BF16])
 @pytest.mark.parametrize("p,cs,offset", [(1, 3 * 1024 * 1024 + 17, 0), (2, 1500, 1), (1, 1024 * 1100, 2)])
 def test_onebit_vs_oracle(bc, oracle_c, dtype, p, cs, offset):

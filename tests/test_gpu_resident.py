@@ -7,7 +7,7 @@ buffer with the C oracle (the reference's compress, K:533-571).  Covered:
 every dtype, p = 1 / 3 (idle workgroups: the CU count is not a multiple of
 3) / 8, a target chunk, ragged chunk sizes (scalar heads and tails), NaN / Inf / signed zeros, every kernel
 configuration, the give-up path (timeout 0: workgroups that see an
-incomplete exchange exit and the fixup kernel quantises their slices),
+incomplete exchange re-read the missing slices themselves),
 back-to-back launches on one stream (tags advance) and launches on two
 streams (separate slots).
 """
@@ -113,7 +113,7 @@ def test_resident_every_configuration(K, oracle_c, env, cfg):
 @pytest.mark.parametrize("dtype", [F32, F16])
 def test_resident_give_up_path(K, oracle_c, env, dtype):
     """timeout 0: a workgroup that does not find every partial on its first
-    sweep gives up; the fixup kernel must produce the same bytes."""
+    sweep gives up and folds the missing slices from memory: same bytes."""
     env["BAGUA_RESIDENT_TIMEOUT_US"] = "0"
     for p in (1, 3):
         x = make_input(p * (1 << 22), dtype, seed=40 + p)
