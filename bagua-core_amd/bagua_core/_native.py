@@ -83,6 +83,10 @@ KERNEL_SIGNATURES = {
     "bagua_onebit_decompress": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _vp]),
     "bagua_onebit_reduce_requantize": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _vp, _sz, _i32, _vp, _sz,
                                               _vp]),
+    "bagua_onebit_piece_range": (_i32, [_i32, _i32, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    "bagua_onebit_encode_range": (_i32, [_i32, _vp, _i32, _i32, _i32, _vp, _sz, _vp, _sz, _i32, _i32, _vp]),
+    "bagua_onebit_finalize": (_i32, [_vp, _sz, _i32, _i32, _i32, _vp, _sz, _vp]),
+    "bagua_onebit_decompress_range": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _i32, _vp]),
     "bagua_reduce_chunks": (_i32, [_i32, _vp, _i32, _i32, _i32, _i32, _vp]),
     "bagua_add_inplace": (_i32, [_i32, _vp, _vp, _i32, _vp]),
     "bagua_addmul_inplace": (_i32, [_i32, _vp, _vp, _i32, _f32, _vp]),

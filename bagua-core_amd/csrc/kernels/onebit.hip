@@ -14,6 +14,7 @@
 // 64-lane xor butterfly per tile, then the same 1024-tree over the tile
 // partials), so the encoder is single-pass over the input and its result is
 // independent of grid size and bit-reproducible against the oracle.
+#include <cstdint>
 #include <type_traits>
 
 #include "codec_common.hpp"
@@ -102,7 +103,8 @@ __device__ __forceinline__ float lane_tree(const float (&a)[4][4]) {
 template <typename T>
 __global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
     const typename T::storage* __restrict__ in, int64_t in_num_elem, int64_t cs, int target,
-    uint8_t* __restrict__ out, int64_t chunk_offset, float* __restrict__ partials, int64_t tiles_per_chunk) {
+    uint8_t* __restrict__ out, int64_t chunk_offset, float* __restrict__ partials, int64_t tiles_per_chunk,
+    int64_t t_begin, int64_t t_end) {
     using S = typename T::storage;
     const int c = target < 0 ? (int)blockIdx.y : target;
     const int64_t n = ob_valid(in_num_elem, cs, c);
@@ -116,7 +118,7 @@ __global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
     // a lane reads 4 consecutive elements per sub-tile: 16 B for f32 but only 8 B
     // for 16-bit types, so those take two tiles per iteration (8 loads in flight)
     constexpr int TPI = 2;
-    for (int64_t t0 = wave * TPI; t0 < tiles_per_chunk; t0 += nwaves * TPI) {
+    for (int64_t t0 = t_begin + wave * TPI; t0 < t_end; t0 += nwaves * TPI) {
         float a[TPI][4][4];
         if (vec && (t0 + TPI) * kObTile <= n) {
             // full tiles: every load issued unconditionally before any is used (a
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
 #pragma unroll
         for (int u = 0; u < TPI; ++u) {
             const int64_t t = t0 + u;
-            if (t >= tiles_per_chunk) break;
+            if (t >= t_end) break;
             // the lane's 16 sign bits form its own 16-bit field (bit sub*4+e)
             uint32_t field = 0;
 #pragma unroll
@@ -266,7 +268,8 @@ __global__ __launch_bounds__(kObFinalizeThreads) void onebit_finalize_kernel(
 // ------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(kBlock) void onebit_decode_kernel(const uint8_t* __restrict__ in, int64_t chunk_offset,
-                                                              int64_t cs, typename T::storage* __restrict__ out) {
+                                                              int64_t cs, typename T::storage* __restrict__ out,
+                                                              int64_t t_begin, int64_t t_end) {
     using S = typename T::storage;
     const int c = blockIdx.y;
     const uint8_t* seg = in + (int64_t)c * chunk_offset;
@@ -276,11 +279,10 @@ __global__ __launch_bounds__(kBlock) void onebit_decode_kernel(const uint8_t* __
     S* dst = out + (int64_t)c * cs;
     const bool vec = ((uintptr_t)dst % (4 * sizeof(S))) == 0;
     const int lane = lane_id();
-    const int64_t tiles = (cs + kObTile - 1) / kObTile;
     const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     const uint32_t sbits = __float_as_uint(scale);
-    for (int64_t t = wave; t < tiles; t += nwaves) {
+    for (int64_t t = t_begin + wave; t < t_end; t += nwaves) {
         // the lane's own 16-bit field: no cross-lane traffic
         const uint32_t field = reinterpret_cast<const uint16_t*>(bits + t * kObTileBytes)[lane];
 #pragma unroll
@@ -387,11 +389,17 @@ static int ob_blocks(int64_t tiles, int nact) {
     return (int)(b < 1 ? 1 : b);
 }
 
+// stage 0: encode every tile + finalize; 1: encode tiles [t_begin, t_end) only
+// (bits + |x| partials, no header); 2: finalize only (header + slack from the
+// partials every stage-1 range left in the workspace)
 template <typename T>
 static int ob_compress_impl(const void* input, int in_num_elem, int cs, int p, uint8_t* out, size_t out_bytes,
-                            void* ws, size_t ws_bytes, int target, hipStream_t s) {
+                            void* ws, size_t ws_bytes, int target, hipStream_t s, int stage = 0,
+                            int64_t t_begin = 0, int64_t t_end = INT64_MAX) {
     using S = typename T::storage;
-    if (p <= 0 || p > 65535 || cs < 0 || target < -1 || target >= p || !input || !out) return BAGUA_ERR_INVALID_ARG;
+    if (p <= 0 || p > 65535 || cs < 0 || target < -1 || target >= p || !out || (!input && stage != 2) ||
+        t_begin < 0 || t_end < t_begin)
+        return BAGUA_ERR_INVALID_ARG;
     const int64_t co = (int64_t)(out_bytes / (size_t)p);
     const int64_t tiles = ob_tiles(cs);
     if (co < 32 + tiles * kObTileBytes) return BAGUA_ERR_INVALID_ARG;
@@ -399,26 +407,30 @@ static int ob_compress_impl(const void* input, int in_num_elem, int cs, int p, u
     if (!ws || ws_bytes < (size_t)nact * (size_t)(tiles > 0 ? tiles : 1) * sizeof(float)) return BAGUA_ERR_WORKSPACE;
     if (((uintptr_t)out + 32) % 4 || co % 4) return BAGUA_ERR_INVALID_ARG;  // bit tiles are written as dwords
     float* partials = static_cast<float*>(ws);
-    if (tiles > 0)
-        launch(onebit_encode_kernel<T>, dim3(ob_blocks(tiles, nact), nact), dim3(kBlock), 0, s,
-                           static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, out, co, partials,
-                           tiles);
-    launch(onebit_finalize_kernel, dim3(nact), dim3(kObFinalizeThreads), 0, s, partials, tiles,
-                       (int64_t)in_num_elem, (int64_t)cs, target, out, co, (int64_t)out_bytes, p);
+    const int64_t tb = stage == 2 ? 0 : t_begin, te = stage == 2 ? tiles : (t_end < tiles ? t_end : tiles);
+    if (stage != 2 && te > tb)
+        launch(onebit_encode_kernel<T>, dim3(ob_blocks(te - tb, nact), nact), dim3(kBlock), 0, s,
+               static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, out, co, partials, tiles, tb,
+               te);
+    if (stage != 1)
+        launch(onebit_finalize_kernel, dim3(nact), dim3(kObFinalizeThreads), 0, s, partials, tiles,
+               (int64_t)in_num_elem, (int64_t)cs, target, out, co, (int64_t)out_bytes, p);
     return check_launch();
 }
 
 template <typename T>
-static int ob_decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, hipStream_t s) {
+static int ob_decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, hipStream_t s,
+                              int64_t t_begin = 0, int64_t t_end = INT64_MAX) {
     using S = typename T::storage;
-    if (p <= 0 || p > 65535 || cs < 0 || !in || !out) return BAGUA_ERR_INVALID_ARG;
+    if (p <= 0 || p > 65535 || cs < 0 || !in || !out || t_begin < 0 || t_end < t_begin) return BAGUA_ERR_INVALID_ARG;
     const int64_t co = (int64_t)(in_bytes / (size_t)p);
     const int64_t tiles = ob_tiles(cs);
     if (co < 32 + tiles * kObTileBytes) return BAGUA_ERR_INVALID_ARG;
     if (((uintptr_t)in + 32) % 4 || co % 4) return BAGUA_ERR_INVALID_ARG;
-    if (tiles == 0) return BAGUA_OK;
-    launch(onebit_decode_kernel<T>, dim3(ob_blocks(tiles, p), p), dim3(kBlock), 0, s, in, co,
-                       (int64_t)cs, static_cast<S*>(out));
+    const int64_t te = t_end < tiles ? t_end : tiles;
+    if (te <= t_begin) return BAGUA_OK;
+    launch(onebit_decode_kernel<T>, dim3(ob_blocks(te - t_begin, p), p), dim3(kBlock), 0, s, in, co, (int64_t)cs,
+           static_cast<S*>(out), t_begin, te);
     return check_launch();
 }
 
@@ -511,6 +523,56 @@ int bagua_onebit_decompress(int dtype, const uint8_t* input, size_t input_bytes,
         case BAGUA_DTYPE_F32: return ob_decompress_impl<F32>(input, input_bytes, chunk_size, num_chunks, output, s);
         case BAGUA_DTYPE_F16: return ob_decompress_impl<F16>(input, input_bytes, chunk_size, num_chunks, output, s);
         case BAGUA_DTYPE_BF16: return ob_decompress_impl<BF16>(input, input_bytes, chunk_size, num_chunks, output, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+int bagua_onebit_piece_range(int chunk_size, int pieces, int piece, int* tile_begin, int* tile_end) {
+    if (chunk_size < 0 || pieces < 1 || piece < 0 || piece >= pieces || !tile_begin || !tile_end)
+        return BAGUA_ERR_INVALID_ARG;
+    const int64_t tiles = ob_tiles(chunk_size), per = (tiles + pieces - 1) / pieces;
+    const int64_t b = (int64_t)piece * per < tiles ? (int64_t)piece * per : tiles;
+    *tile_begin = (int)b;
+    *tile_end = (int)(b + per < tiles ? b + per : tiles);
+    return BAGUA_OK;
+}
+
+int bagua_onebit_encode_range(int dtype, const void* input, int input_num_element, int chunk_size, int num_chunks,
+                              uint8_t* output, size_t output_bytes, void* workspace, size_t workspace_bytes,
+                              int tile_begin, int tile_end, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return ob_compress_impl<F32>(input, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                         workspace, workspace_bytes, -1, s, 1, tile_begin, tile_end);
+        case BAGUA_DTYPE_F16:
+            return ob_compress_impl<F16>(input, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                         workspace, workspace_bytes, -1, s, 1, tile_begin, tile_end);
+        case BAGUA_DTYPE_BF16:
+            return ob_compress_impl<BF16>(input, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                          workspace, workspace_bytes, -1, s, 1, tile_begin, tile_end);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+int bagua_onebit_finalize(const void* workspace, size_t workspace_bytes, int input_num_element, int chunk_size,
+                          int num_chunks, uint8_t* output, size_t output_bytes, bagua_stream_t stream) {
+    // the header math is dtype-independent (partials are f32)
+    return ob_compress_impl<F32>(nullptr, input_num_element, chunk_size, num_chunks, output, output_bytes,
+                                 const_cast<void*>(workspace), workspace_bytes, -1, static_cast<hipStream_t>(stream), 2);
+}
+
+int bagua_onebit_decompress_range(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                                  int num_chunks, void* output, int tile_begin, int tile_end, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return ob_decompress_impl<F32>(input, input_bytes, chunk_size, num_chunks, output, s, tile_begin, tile_end);
+        case BAGUA_DTYPE_F16:
+            return ob_decompress_impl<F16>(input, input_bytes, chunk_size, num_chunks, output, s, tile_begin, tile_end);
+        case BAGUA_DTYPE_BF16:
+            return ob_decompress_impl<BF16>(input, input_bytes, chunk_size, num_chunks, output, s, tile_begin,
+                                            tile_end);
     }
     return BAGUA_ERR_UNSUPPORTED;
 }

@@ -139,12 +139,13 @@ int env_int(const char* name, long dflt) {
     return v && *v ? (int)std::strtol(v, nullptr, 10) : (int)dflt;
 }
 
-int auto_pieces(size_t cs) {
+int auto_pieces(size_t payload_bytes) {
     // BAGUA_PIPELINE_PIECES caps the count (1 disables), pieces keep at least
-    // BAGUA_PIPELINE_MIN_PIECE elements (the exchange of a piece is p times that)
+    // BAGUA_PIPELINE_MIN_PIECE payload bytes per chunk (= elements for MinMax
+    // u8; the exchange of a piece is p times that)
     const int kmax = env_int("BAGUA_PIPELINE_PIECES", 4);
     const int min_piece = env_int("BAGUA_PIPELINE_MIN_PIECE", 1 << 20);
-    size_t k = cs / (size_t)(min_piece > 0 ? min_piece : 1);
+    size_t k = payload_bytes / (size_t)(min_piece > 0 ? min_piece : 1);
     if (k > (size_t)kmax) k = (size_t)kmax;
     return k < 1 ? 1 : (int)k;
 }
@@ -168,6 +169,16 @@ void piece_bytes(const Chunking& k, int pieces, int q, size_t* lo, size_t* hi) {
     }
     *lo = q == 0 ? 0 : 32 + (size_t)b;
     *hi = (size_t)e == k.cs ? co : 32 + (size_t)e;
+}
+
+// 1-bit segment bytes of tile range [tb, te): header with piece 0 when `header`, the rest
+// of the segment (slack) with the last tile
+void onebit_piece_bytes(const Chunking& k, int tb, int te, bool header, size_t* lo, size_t* hi) {
+    const size_t co = k.S / k.p;
+    const int tiles = (int)((k.cs + 1023) / 1024);
+    *lo = header ? 0 : 32 + (size_t)tb * 128;
+    *hi = te >= tiles ? co : 32 + (size_t)te * 128;
+    if (!header && tb >= te) *lo = *hi = 0;
 }
 
 // one piece of the alltoall (send -> recv) or of the in-place allgather (send)
@@ -213,7 +224,7 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
     Chunking k;
     int rc = plan(c, t, BAGUA_COMPRESSION_MINMAX_UINT8, &k);
     if (rc) return rc;
-    if (pieces < 1) pieces = auto_pieces(k.cs);
+    if (pieces < 1) pieces = k.p == 1 ? 1 : auto_pieces(k.cs);  // one rank: no exchange to hide
     if (pieces == 1 || !pipeline_fits(c, t, k)) return centralized(c, t, average, BAGUA_COMPRESSION_MINMAX_UINT8, true);
     DeviceGuard guard(c->device_id);
     if (c->ensure_side(3 * (size_t)pieces + 1)) return BAGUA_ERR_HIP;
@@ -277,12 +288,88 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
     return finish_both(c, BAGUA_OK);
 }
 
+// The 1-bit op, pipelined the same way.  A 1-bit header (scale) needs the whole
+// chunk's |x| partials, so the alltoall sends the sign bits of piece q as soon
+// as they are encoded and the headers with the last piece; the fused middle
+// step (which needs every received scale) runs once, after the last piece.
+// The allgather sends the headers with piece 0 and the decode of piece q
+// follows its arrival.
+//
+//   stream: E0 E1 .. Ek F | R+F | D0 D1 .. Dk
+//   side  :    A0 A1 .. Ak+hdr   G0+hdr G1 .. Gk
+int centralized_pipelined_onebit(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int average, int pieces) {
+    Chunking k;
+    int rc = plan(c, t, BAGUA_COMPRESSION_ONEBIT, &k);
+    if (rc) return rc;
+    if (pieces < 1) pieces = k.p == 1 ? 1 : auto_pieces(k.cs / 8);  // sign bits per chunk
+    if (pieces == 1 || k.p > 16 || t->num_elem != t->num_elem_allocated || k.cs > 0x7fffffffULL)
+        return centralized(c, t, average, BAGUA_COMPRESSION_ONEBIT, true);
+    DeviceGuard guard(c->device_id);
+    if (c->ensure_side(2 * (size_t)pieces + 2)) return BAGUA_ERR_HIP;
+    hipStream_t s0 = c->stream, s1 = c->side;
+    hipEvent_t* encoded = c->events.data();
+    hipEvent_t* gathered = encoded + pieces;
+    hipEvent_t exchanged = gathered[pieces], requantised = gathered[pieces + 1];
+    const int dt = t->dtype, cs = (int)k.cs, p = k.p;
+    void* x = (void*)(uintptr_t)t->ptr;
+    PoolBuffer send, recv;
+    TRY(send.allocate(c->device_id, k.S));
+    TRY(recv.allocate(c->device_id, k.S));
+    uint8_t* sb = send.as<uint8_t>();
+    uint8_t* rb = recv.as<uint8_t>();
+    const size_t ws_bytes = bagua_onebit_workspace_bytes(cs, p);
+    void* ws = (void*)(uintptr_t)stream_workspace(c->device_id, (uint64_t)(uintptr_t)s0, ws_bytes);
+    if (!ws) return finish(c, BAGUA_ERR_OOM);
+    HIP2(hipEventRecord(requantised, s0));
+    HIP2(hipStreamWaitEvent(s1, requantised, 0));
+    // 1. encode piece by piece (bits + partials of every chunk), headers last
+    for (int q = 0; q < pieces; ++q) {
+        int tb, te;
+        bagua_onebit_piece_range(cs, pieces, q, &tb, &te);
+        if (te > tb) TRY2(bagua_onebit_encode_range(dt, x, (int)t->num_elem, cs, p, sb, k.S, ws, ws_bytes, tb, te, s0));
+        if (q == pieces - 1) TRY2(bagua_onebit_finalize(ws, ws_bytes, (int)t->num_elem, cs, p, sb, k.S, s0));
+        HIP2(hipEventRecord(encoded[q], s0));
+    }
+    for (int q = 0; q < pieces; ++q) {
+        int tb, te;
+        bagua_onebit_piece_range(cs, pieces, q, &tb, &te);
+        size_t lo, hi;
+        onebit_piece_bytes(k, tb, te, false, &lo, &hi);
+        HIP2(hipStreamWaitEvent(s1, encoded[q], 0));
+        TRY2(exchange_piece(c, k, sb, rb, lo, hi, true));
+        if (q == pieces - 1) TRY2(exchange_piece(c, k, sb, rb, 0, 32, true));  // the headers
+    }
+    HIP2(hipEventRecord(exchanged, s1));
+    // 2. decode the p received segments of the own chunk, reduce, re-encode it (not stored)
+    HIP2(hipStreamWaitEvent(s0, exchanged, 0));
+    TRY2(bagua_onebit_reduce_requantize(dt, rb, k.S, cs, p, nullptr, average, sb, k.S, k.rank, ws, ws_bytes, s0));
+    HIP2(hipEventRecord(requantised, s0));
+    // 3. allgather (headers with piece 0) + decode piece by piece
+    HIP2(hipStreamWaitEvent(s1, requantised, 0));
+    for (int q = 0; q < pieces; ++q) {
+        int tb, te;
+        bagua_onebit_piece_range(cs, pieces, q, &tb, &te);
+        size_t lo, hi;
+        onebit_piece_bytes(k, tb, te, q == 0, &lo, &hi);
+        TRY2(exchange_piece(c, k, sb, rb, lo, hi, false));
+        HIP2(hipEventRecord(gathered[q], s1));
+    }
+    for (int q = 0; q < pieces; ++q) {
+        int tb, te;
+        bagua_onebit_piece_range(cs, pieces, q, &tb, &te);
+        HIP2(hipStreamWaitEvent(s0, gathered[q], 0));
+        if (te > tb) TRY2(bagua_onebit_decompress_range(dt, sb, k.S, cs, p, x, tb, te, s0));
+    }
+    return finish_both(c, BAGUA_OK);
+}
+
 }  // namespace
 
 extern "C" {
 
 int bagua_centralized_low_precision_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int average,
                                               int method, int pieces) {
+    if (method == BAGUA_COMPRESSION_ONEBIT) return centralized_pipelined_onebit(c, t, average, pieces);
     if (method != BAGUA_COMPRESSION_MINMAX_UINT8) return centralized(c, t, average, method, true);
     return centralized_pipelined(c, t, average, pieces);
 }

@@ -388,11 +388,12 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     t_f = timed(fp32_step, max(3, args.steps // 2), max(1, args.warmup // 2))
     # the same all-reduce with the 1-bit sign+scale codec (this repo's extension:
     # N/8 wire bytes per phase instead of N), fused middle step
-    def onebit_step():
-        N.check(N.C.bagua_centralized_low_precision_synchronous(comm.handle, ctypes.byref(raw), 1,
-                                                                N.COMPRESSION_ONEBIT), "1-bit allreduce")
+    def onebit_step(pieces=args.pieces):
+        N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
+                                                              N.COMPRESSION_ONEBIT, pieces), "1-bit allreduce")
 
     t_o = timed(onebit_step, max(3, args.steps // 2), max(1, args.warmup // 2))
+    t_ou = timed(lambda: onebit_step(1), max(3, args.steps // 2), max(1, args.warmup // 2))
     decentralized = None
     if not args.no_decentralized:
         # config 5: bf16 bucket, decentralized ring exchange with the uint8 codec
@@ -462,7 +463,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
              "ratio_vs_fp32": round(per_rank / fp32, 3), "fp32_ms_per_step": round(t_f * 1e3, 3),
              "pieces": args.pieces or "auto", "unpieced_ms_per_step": round(t_u * 1e3, 3),
              "decentralized_bf16": decentralized,
-             "onebit_allreduce": {"ms_per_step": round(t_o * 1e3, 3),
+             "onebit_allreduce": {"ms_per_step": round(t_o * 1e3, 3), "unpieced_ms_per_step": round(t_ou * 1e3, 3),
                                   "per_rank_gib_s": round(4.0 * n / t_o / GiB, 2),
                                   "ratio_vs_fp32": round((4.0 * n / t_o) / (4.0 * n / t_f), 3)},
              "per_kernel_us": {nm: round(t * 1e3, 2) for nm, t in zip(names, per)}}

@@ -99,6 +99,22 @@ int bagua_onebit_compress(int dtype, const void* input, int input_num_element, i
                           size_t workspace_bytes, int target_chunk, bagua_stream_t stream);
 int bagua_onebit_decompress(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
                             int num_chunks, void* output, bagua_stream_t stream);
+/* Pieced 1-bit codec (the pipelined centralized op): a chunk's 1024-element
+ * tiles split into `pieces` tile ranges (bagua_onebit_piece_range; trailing
+ * ranges may be empty).  bagua_onebit_encode_range writes the sign bits and
+ * |x| tile partials (workspace) of tiles [tile_begin, tile_end) of EVERY chunk
+ * and no header; once every range is encoded, bagua_onebit_finalize writes the
+ * headers (scale, count) and slack from the partials: together exactly the
+ * bytes of bagua_onebit_compress (target -1).  bagua_onebit_decompress_range
+ * decodes tiles [tile_begin, tile_end) of every chunk (headers present). */
+int bagua_onebit_piece_range(int chunk_size, int pieces, int piece, int* tile_begin, int* tile_end);
+int bagua_onebit_encode_range(int dtype, const void* input, int input_num_element, int chunk_size, int num_chunks,
+                              uint8_t* output, size_t output_bytes, void* workspace, size_t workspace_bytes,
+                              int tile_begin, int tile_end, bagua_stream_t stream);
+int bagua_onebit_finalize(const void* workspace, size_t workspace_bytes, int input_num_element, int chunk_size,
+                          int num_chunks, uint8_t* output, size_t output_bytes, bagua_stream_t stream);
+int bagua_onebit_decompress_range(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                                  int num_chunks, void* output, int tile_begin, int tile_end, bagua_stream_t stream);
 /* Middle step of the centralized op with the 1-bit codec, fused: decode the
  * num_chunks received segments of `input`, reduce them into chunk
  * `target_chunk` of `tensor` in the reference's summation order (mean if

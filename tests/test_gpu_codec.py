@@ -277,6 +277,43 @@ def test_onebit_fused_reduce_requantize(bc, oracle_c, dtype, p, store):
     assert np.array_equal(segment_bytes(send_d.cpu().numpy(), p, r), segment_bytes(send_want, p, r))
 
 
+@pytest.mark.parametrize("dtype", [F32, F16, BF16])
+@pytest.mark.parametrize("p,cs,pieces,offset", [(1, 5 * 1024 + 17, 3, 0), (3, 4096, 5, 1), (2, 100000, 4, 0),
+                                                (4, 700, 2, 0)])
+def test_onebit_piecewise_building_blocks(bc, oracle_c, dtype, p, cs, pieces, offset):
+    """encode_range over every piece + finalize == bagua_onebit_compress; decompress_range over
+    every piece == bagua_onebit_decompress (the pipelined op's building blocks)."""
+    from oracle import oracle_np as NP
+    rng = np.random.default_rng(cs + p + pieces)
+    x = NP.from_f32((rng.standard_normal(p * cs) * 1e-3).astype(np.float32), dtype)
+    want = oracle_c.compress_onebit(x, dtype, p)
+    K = bc._native.K
+    xt = to_dev(x, dtype, offset)
+    S = K.bagua_onebit_compressed_bytes(cs, p)
+    assert S == want.size
+    out = torch.full((S,), 0x5A, dtype=torch.uint8, device="cuda")
+    wsb = K.bagua_onebit_workspace_bytes(cs, p)
+    ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+    b, e = ctypes.c_int(), ctypes.c_int()
+    ranges = []
+    for q in range(pieces):
+        assert K.bagua_onebit_piece_range(cs, pieces, q, ctypes.byref(b), ctypes.byref(e)) == 0
+        ranges.append((b.value, e.value))
+        assert K.bagua_onebit_encode_range(dtype, xt.data_ptr(), p * cs, cs, p, out.data_ptr(), S, ws.data_ptr(), wsb,
+                                           b.value, e.value, None) == 0
+    tiles = (cs + 1023) // 1024
+    assert ranges[0][0] == 0 and ranges[-1][1] == tiles
+    assert all(ranges[i][1] == ranges[i + 1][0] for i in range(pieces - 1))
+    assert K.bagua_onebit_finalize(ws.data_ptr(), wsb, p * cs, cs, p, out.data_ptr(), S, None) == 0
+    assert np.array_equal(out.cpu().numpy(), want)
+    dec = torch.zeros(p * cs, dtype=TORCH[dtype], device="cuda")
+    for tb, te in ranges:
+        assert K.bagua_onebit_decompress_range(dtype, out.data_ptr(), S, cs, p, dec.data_ptr(), tb, te, None) == 0
+    dw = np.zeros(p * cs, STORAGE[dtype])
+    oracle_c.decompress_onebit(want, p, dw, dtype)
+    assert_float_bits_equal(to_host(dec, dtype), dw, dtype, "pieced 1-bit decode")
+
+
 @pytest.mark.parametrize("dtype", [F32, BF16])
 @pytest.mark.parametrize("p,cs,offset", [(1, 3 * 1024 * 1024 + 17, 0), (2, 1500, 1), (1, 1024 * 1100, 2)])
 def test_onebit_vs_oracle(bc, oracle_c, dtype, p, cs, offset):

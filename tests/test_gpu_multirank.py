@@ -113,6 +113,34 @@ def test_centralized_pipelined_multirank(bc, oracle_c, p, dtype, cs, pieces):
         assert np.array_equal(host(ts[r], dtype).view(np.uint8), want[r].view(np.uint8)), f"rank {r}"
 
 
+@pytest.mark.parametrize("p,dtype,cs,pieces", [(2, F32, 4096 * 3, 3), (4, F32, 40000, 4), (8, BF16, 2500 * 4, 2),
+                                               (8, F32, 5000 * 8, 5), (4, F16, 1024 * 7 + 3, 3), (1, F32, 70000, 3),
+                                               (16, F32, 3000 * 2, 2), (3, F32, 2048, 4), (2, F32, 0, 2),
+                                               (2, F32, (1 << 24) + 1000, 0)])
+def test_centralized_onebit_pipelined_multirank(bc, oracle_c, p, dtype, cs, pieces):
+    """Pieced 1-bit op (sign bits of piece q exchanged while piece q+1 encodes, headers with
+    the last alltoall piece and the first allgather piece) == the reference op sequence with the
+    1-bit codec, every rank bit-for-bit.  (3, F32, 2048, 4): 2 tiles, empty trailing pieces;
+    cs = 0: headers only; pieces = 0: automatic (4 pieces of >= 1 MiB of bits per chunk)."""
+    from bagua_core.communicator import loopback_communicators
+    rng = np.random.default_rng(p * 77 + cs + dtype)
+    xs = [NP.from_f32((rng.standard_normal(p * cs) * 1e-3 - 3e-4 * r).astype(np.float32), dtype) for r in range(p)]
+    want = simulate.centralized_low_precision(oracle_c, xs, dtype, True, method="OneBitSignScale")
+    comms = loopback_communicators(p, 0)
+    ts = [dev(x, dtype) for x in xs]
+    torch.cuda.synchronize()
+    N = bc._native
+
+    def rank(r):
+        raw = bc.BaguaTensorPy(ts[r], "g").raw()
+        N.check(N.C.bagua_centralized_low_precision_pipelined(comms[r].handle, ctypes.byref(raw), 1,
+                                                              N.COMPRESSION_ONEBIT, pieces), f"rank {r}")
+
+    run_ranks(rank, p)
+    for r in range(p):
+        assert np.array_equal(host(ts[r], dtype).view(np.uint8), want[r].view(np.uint8)), f"rank {r}"
+
+
 @pytest.mark.parametrize("p,dtype,short", [(2, F32, 37), (4, BF16, 1000), (3, F32, 4096 + 5)])
 def test_centralized_partially_valid_tensor(bc, oracle_c, p, dtype, short):
     """num_elem < num_elem_allocated: the reference compresses num_elements()
