@@ -11,11 +11,12 @@
  *   DT  = bagua-core-internal/src/datatypes/mod.rs
  *   CUB = bagua-core-internal/third_party/cub-1.8.0/cub
  *
- * Parity pin: the reference ships no golden vectors, KATs or tests for this
- * path and cannot be built or imported here (F5).  This C
- * restatement is pinned by (1) source reading with line citations, and (2)
- * an independently written numpy restatement (oracle/oracle_np.py) that must
- * agree with it bit-for-bit on every committed fixture (tests/golden/).
+ * PARITY UNPINNED: the reference ships no golden vectors, KATs or tests for
+ * this path and cannot be built or imported here (F5), so no
+ * reference output pins this restatement.  It rests on (1) source reading
+ * with line citations, and (2) an independently written numpy restatement
+ * (oracle/oracle_np.py) that must agree with it bit-for-bit on every
+ * committed fixture (tests/golden/).
  * bf16 (F2) and the 1-bit sign+scale codec (F1) have no reference
  * counterpart: their formats are defined by this repository and
  * are "parity unpinned" with respect to the reference.

@@ -23,7 +23,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("minmax_resident_encode_kernel", "minmax_resident_fixup_kernel",
+KERNELS = ("minmax_resident_encode_kernel",
            "minmax_partials_kernel", "minmax_quantize_kernel", "minmax_dequantize_kernel",
            "onebit_encode_kernel", "onebit_decode_kernel", "dequant_reduce_kernel")
 

@@ -27,6 +27,12 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --two-pass > /dev/null
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_2p" -o run -- \
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --two-pass > /dev/null
+# plain bench lines (no profiler) for the committed r*_b_*.json
+timeout -k 10 200 python3 bench.py > "$OUT/b_codec.json"
+timeout -k 10 120 python3 bench.py --workload onebit --no-cpu-baseline > "$OUT/b_onebit.json"
+timeout -k 10 120 python3 bench.py --dtype bf16 --no-cpu-baseline > "$OUT/b_codec_bf16.json"
+timeout -k 10 120 python3 bench.py --workload allreduce > "$OUT/b_ar1.json"
+timeout -k 10 200 python3 bench.py --workload host --steps 10 > "$OUT/b_host.json"
 # python3 profiles/collect_pmc.py "$OUT/fetch" "$OUT/write" "profiles/${R}_pmc_traffic.json"
 # (run locally on the merged gpurun_out/: only gpurun_out/ returns from the box)
 # cp "$(find "$OUT/trace" -name '*kernel_stats.csv' | head -1)" "profiles/${R}_bench_n1_kernel_stats.csv"
