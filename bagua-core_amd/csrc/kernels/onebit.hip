@@ -15,6 +15,7 @@
 // partials), so the encoder is single-pass over the input and its result is
 // independent of grid size and bit-reproducible against the oracle.
 #include <cstdint>
+#include <cstdlib>
 #include <type_traits>
 
 #include "codec_common.hpp"
@@ -25,6 +26,11 @@ namespace bagua {
 constexpr int kObTile = 1024;
 constexpr int kObTileBytes = 128;
 constexpr int kObFinalizeThreads = 1024;
+// encode grid cap: 1024 workgroups (4 per CU) with 64 B of loads in flight per
+// lane (one tile per iteration for 32-bit types, two for 16-bit ones) beat
+// 2048 workgroups and 2 tiles by 3 % (f32) to 5 % (bf16) on the 256 MiB step
+// (profiles/r01_onebit_shape_sweep.jsonl)
+constexpr int kObEncodeBlocks = 1024;
 
 __device__ __forceinline__ int64_t ob_valid(int64_t in_num_elem, int64_t cs, int c) {
     int64_t r = in_num_elem - (int64_t)c * cs;
@@ -100,7 +106,7 @@ __device__ __forceinline__ float lane_tree(const float (&a)[4][4]) {
 // ------------------------------------------------------------------------
 // encode: bits + per-tile |x| partials, one wave per tile
 // ------------------------------------------------------------------------
-template <typename T>
+template <typename T, int TPI>
 __global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
     const typename T::storage* __restrict__ in, int64_t in_num_elem, int64_t cs, int target,
     uint8_t* __restrict__ out, int64_t chunk_offset, float* __restrict__ partials, int64_t tiles_per_chunk,
@@ -116,8 +122,8 @@ __global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
     const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     // a lane reads 4 consecutive elements per sub-tile: 16 B for f32 but only 8 B
-    // for 16-bit types, so those take two tiles per iteration (8 loads in flight)
-    constexpr int TPI = 2;
+    // for 16-bit types, so those take TPI = 2 tiles per iteration (64 B in flight
+    // per lane either way)
     for (int64_t t0 = t_begin + wave * TPI; t0 < t_end; t0 += nwaves * TPI) {
         float a[TPI][4][4];
         if (vec && (t0 + TPI) * kObTile <= n) {
@@ -382,9 +388,9 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_kernel(
 // ------------------------------------------------------------------------
 static int64_t ob_tiles(int64_t cs) { return (cs + kObTile - 1) / kObTile; }
 
-static int ob_blocks(int64_t tiles, int nact) {
+static int ob_blocks(int64_t tiles, int nact, int target_blocks = kTargetBlocks) {
     int64_t b = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    const int64_t cap = (kTargetBlocks + nact - 1) / nact;
+    const int64_t cap = (target_blocks + nact - 1) / nact;
     if (b > cap) b = cap;
     return (int)(b < 1 ? 1 : b);
 }
@@ -409,9 +415,9 @@ static int ob_compress_impl(const void* input, int in_num_elem, int cs, int p, u
     float* partials = static_cast<float*>(ws);
     const int64_t tb = stage == 2 ? 0 : t_begin, te = stage == 2 ? tiles : (t_end < tiles ? t_end : tiles);
     if (stage != 2 && te > tb)
-        launch(onebit_encode_kernel<T>, dim3(ob_blocks(te - tb, nact), nact), dim3(kBlock), 0, s,
-               static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, out, co, partials, tiles, tb,
-               te);
+        launch(onebit_encode_kernel<T, sizeof(S) == 4 ? 1 : 2>, dim3(ob_blocks(te - tb, nact, kObEncodeBlocks), nact),
+               dim3(kBlock), 0, s, static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, out, co,
+               partials, tiles, tb, te);
     if (stage != 1)
         launch(onebit_finalize_kernel, dim3(nact), dim3(kObFinalizeThreads), 0, s, partials, tiles,
                (int64_t)in_num_elem, (int64_t)cs, target, out, co, (int64_t)out_bytes, p);
