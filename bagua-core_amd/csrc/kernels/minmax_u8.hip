@@ -227,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
 // ------------------------------------------------------------------------
 // dequantise
 // ------------------------------------------------------------------------
-template <typename T>
+template <typename T, bool NTS = true>
 __global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
     const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int64_t e0, int64_t e1,
     typename T::storage* __restrict__ out) {
@@ -270,7 +270,8 @@ __global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
                 split_bytes<T>(raw[k], b);
 #pragma unroll
                 for (int i = 0; i < N; ++i) b[i] = lut[b[i]];
-                nt_store16(pack_stored<T>(b), &vdst[base + k * kBlock + threadIdx.x]);
+                if constexpr (NTS) nt_store16(pack_stored<T>(b), &vdst[base + k * kBlock + threadIdx.x]);
+                else vdst[base + k * kBlock + threadIdx.x] = pack_stored<T>(b);
             }
             continue;
         }
@@ -281,7 +282,8 @@ __global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
             split_bytes<T>(load_word<T>(vsrc + v * N), b);
 #pragma unroll
             for (int i = 0; i < N; ++i) b[i] = lut[b[i]];
-            nt_store16(pack_stored<T>(b), &vdst[v]);
+            if constexpr (NTS) nt_store16(pack_stored<T>(b), &vdst[v]);
+            else vdst[v] = pack_stored<T>(b);
         }
     }
     if (blockIdx.x == 0) {
@@ -434,9 +436,11 @@ static int decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p, vo
     if (p <= 0 || p > 65535 || cs < 0 || !in || !out || e0 < 0 || e1 < e0 || e1 > cs) return BAGUA_ERR_INVALID_ARG;
     const int64_t chunk_offset = (int64_t)(in_bytes / (size_t)p);  // K:566
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
-    launch(minmax_dequantize_kernel<T>,
-                       dim3(blocks_for(e1 - e0, Vec<T>::N, p, kSubtiles, kDequantBlocks), p), dim3(kBlock), 0,
-                       s, in, chunk_offset, (int64_t)cs, (int64_t)e0, (int64_t)e1, static_cast<S*>(out));
+    // nt stores: with default-policy stores the decoded bucket's dirty lines sit in the
+    // Infinity Cache and the next encode's pass 2 pays for them (85 -> 119 us per
+    // 256 MiB encode)
+    launch(minmax_dequantize_kernel<T, true>, dim3(blocks_for(e1 - e0, Vec<T>::N, p, kSubtiles, kDequantBlocks), p),
+           dim3(kBlock), 0, s, in, chunk_offset, (int64_t)cs, (int64_t)e0, (int64_t)e1, static_cast<S*>(out));
     return check_launch();
 }
 

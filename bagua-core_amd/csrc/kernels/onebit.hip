@@ -69,17 +69,20 @@ __device__ __forceinline__ void unpack4(const uint2& v, float (&f)[4]) {
     f[2] = T::to_f((uint16_t)(v.y & 0xffff)); f[3] = T::to_f((uint16_t)(v.y >> 16));
 }
 
-template <typename T>
+template <typename T, bool NTS = true>
 __device__ __forceinline__ void store4(typename T::storage* p, int64_t j, int64_t n, bool vec, const float (&f)[4]) {
     using S = typename T::storage;
     if (vec && j + 4 <= n) {
         if constexpr (sizeof(S) == 4) {
-            nt_store16(make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3])), p + j);
+            const uint4 v = make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+            if constexpr (NTS) nt_store16(v, p + j);
+            else *reinterpret_cast<uint4*>(p + j) = v;
         } else {
             uint2 v;
             v.x = (uint32_t)T::from_f(f[0]) | ((uint32_t)T::from_f(f[1]) << 16);
             v.y = (uint32_t)T::from_f(f[2]) | ((uint32_t)T::from_f(f[3]) << 16);
-            nt_store8(v, p + j);
+            if constexpr (NTS) nt_store8(v, p + j);
+            else *reinterpret_cast<uint2*>(p + j) = v;
         }
         return;
     }
@@ -106,7 +109,7 @@ __device__ __forceinline__ float lane_tree(const float (&a)[4][4]) {
 // ------------------------------------------------------------------------
 // encode: bits + per-tile |x| partials, one wave per tile
 // ------------------------------------------------------------------------
-template <typename T, int TPI>
+template <typename T, int TPI, bool NTL = true>
 __global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
     const typename T::storage* __restrict__ in, int64_t in_num_elem, int64_t cs, int target,
     uint8_t* __restrict__ out, int64_t chunk_offset, float* __restrict__ partials, int64_t tiles_per_chunk,
@@ -136,8 +139,8 @@ __global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const S* p = src + (t0 + u) * kObTile + k * 256 + lane * 4;
-                    if constexpr (sizeof(S) == 4) raw[u][k] = nt_load16(p);
-                    else raw[u][k] = nt_load8(p);
+                    if constexpr (sizeof(S) == 4) raw[u][k] = NTL ? nt_load16(p) : *reinterpret_cast<const uint4*>(p);
+                    else raw[u][k] = NTL ? nt_load8(p) : *reinterpret_cast<const uint2*>(p);
                 }
 #pragma unroll
             for (int u = 0; u < TPI; ++u)
@@ -272,7 +275,7 @@ __global__ __launch_bounds__(kObFinalizeThreads) void onebit_finalize_kernel(
 // ------------------------------------------------------------------------
 // decode
 // ------------------------------------------------------------------------
-template <typename T>
+template <typename T, bool NTS>
 __global__ __launch_bounds__(kBlock) void onebit_decode_kernel(const uint8_t* __restrict__ in, int64_t chunk_offset,
                                                               int64_t cs, typename T::storage* __restrict__ out,
                                                               int64_t t_begin, int64_t t_end) {
@@ -297,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void onebit_decode_kernel(const uint8_t* __
 #pragma unroll
             for (int e = 0; e < 4; ++e)  // bit ? -scale : +scale, as a sign-bit flip
                 f[e] = __uint_as_float(sbits ^ ((field << (31 - (k * 4 + e))) & 0x80000000u));
-            store4<T>(dst, t * kObTile + k * 256 + lane * 4, cs, vec, f);
+            store4<T, NTS>(dst, t * kObTile + k * 256 + lane * 4, cs, vec, f);
         }
     }
 }
@@ -414,10 +417,13 @@ static int ob_compress_impl(const void* input, int in_num_elem, int cs, int p, u
     if (((uintptr_t)out + 32) % 4 || co % 4) return BAGUA_ERR_INVALID_ARG;  // bit tiles are written as dwords
     float* partials = static_cast<float*>(ws);
     const int64_t tb = stage == 2 ? 0 : t_begin, te = stage == 2 ? tiles : (t_end < tiles ? t_end : tiles);
+    // nt loads: default-policy loads behind the decode's default-policy stores take
+    // 77 us instead of 47 (profiles/r01_decode_store_ab.jsonl)
     if (stage != 2 && te > tb)
-        launch(onebit_encode_kernel<T, sizeof(S) == 4 ? 1 : 2>, dim3(ob_blocks(te - tb, nact, kObEncodeBlocks), nact),
-               dim3(kBlock), 0, s, static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, out, co,
-               partials, tiles, tb, te);
+        launch(onebit_encode_kernel<T, sizeof(S) == 4 ? 1 : 2, true>,
+               dim3(ob_blocks(te - tb, nact, kObEncodeBlocks), nact), dim3(kBlock), 0, s,
+               static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, out, co, partials, tiles, tb,
+               te);
     if (stage != 1)
         launch(onebit_finalize_kernel, dim3(nact), dim3(kObFinalizeThreads), 0, s, partials, tiles,
                (int64_t)in_num_elem, (int64_t)cs, target, out, co, (int64_t)out_bytes, p);
@@ -435,8 +441,10 @@ static int ob_decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p,
     if (((uintptr_t)in + 32) % 4 || co % 4) return BAGUA_ERR_INVALID_ARG;
     const int64_t te = t_end < tiles ? t_end : tiles;
     if (te <= t_begin) return BAGUA_OK;
-    launch(onebit_decode_kernel<T>, dim3(ob_blocks(te - t_begin, p), p), dim3(kBlock), 0, s, in, co, (int64_t)cs,
-           static_cast<S*>(out), t_begin, te);
+    // default-policy stores: 43 us vs 50 us with nt stores per 256 MiB decode, and the
+    // next encode (nt loads) is unaffected (profiles/r01_decode_store_ab.jsonl)
+    launch(onebit_decode_kernel<T, false>, dim3(ob_blocks(te - t_begin, p), p), dim3(kBlock), 0, s, in, co,
+           (int64_t)cs, static_cast<S*>(out), t_begin, te);
     return check_launch();
 }
 

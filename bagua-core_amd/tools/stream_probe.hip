@@ -2,7 +2,7 @@
 // on gfx950, timed with hipEvents, interleaved rounds in one process
 // (cdna_hip_programming.md §5.4 rule 24).  f32, 256 MiB, aligned.
 //
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include -ffp-contract=off \
 //         -fhip-fp32-correctly-rounded-divide-sqrt -o stream_probe stream_probe.hip
 #include <hip/hip_runtime.h>
 
@@ -253,6 +253,7 @@ __global__ __launch_bounds__(256) void minmax_k(const u32x4* __restrict__ in, ui
 
 // the product kernels, compiled into this TU for side-by-side timing
 #include "../csrc/kernels/minmax_u8.hip"
+#include "../csrc/kernels/minmax_resident.hip"
 #include "../csrc/kernels/reduce.hip"
 #include "../csrc/kernels/status.cpp"
 
@@ -339,7 +340,7 @@ int main(int argc, char** argv) {
         bagua_minmax_u8_decompress(0, comp, S, (int)n, 1, y, nullptr); });
     add("PRODUCT dequantize raw-launch g2048", B + W, [=](int) {
         hipLaunchKernelGGL(bagua::minmax_dequantize_kernel<bagua::F32>, dim3(2048, 1), dim3(256), 0, nullptr,
-                           comp, (int64_t)S, (int64_t)n, (float*)y); });
+                           comp, (int64_t)S, (int64_t)n, (int64_t)0, (int64_t)n, (float*)y); });
     float* hdr;
     CK(hipMalloc(&hdr, 16));
     {
