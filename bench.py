@@ -392,6 +392,20 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
                                                               N.COMPRESSION_ONEBIT, pieces), "1-bit allreduce")
 
+    # decomposition: the op's two collectives alone on its compressed bytes (RCCL alltoall of
+    # S bytes, in-place allgather of S bytes), so the codec time the op did not hide is
+    # ms_per_step - comm_only_ms
+    S_c = N.K.bagua_minmax_u8_compressed_bytes(0, n // world, world)
+    cbuf = [torch.zeros(S_c, dtype=torch.uint8, device=dev) for _ in range(2)]
+    craw = [N.bagua_tensor_t(b.data_ptr(), S_c, S_c, 3, local_rank) for b in cbuf]
+
+    def comm_only():
+        N.check(N.C.bagua_comm_alltoall(comm.handle, ctypes.byref(craw[0]), ctypes.byref(craw[1])), "alltoall")
+        N.check(N.C.bagua_comm_allgather_inplace(comm.handle, ctypes.byref(craw[1])), "allgather")
+        N.check(N.C.bagua_comm_synchronize(comm.handle), "sync")
+
+    t_comm = timed(comm_only, max(3, args.steps // 2), max(1, args.warmup // 2))
+    del cbuf, craw
     t_o = timed(onebit_step, max(3, args.steps // 2), max(1, args.warmup // 2))
     t_ou = timed(lambda: onebit_step(1), max(3, args.steps // 2), max(1, args.warmup // 2))
     decentralized = None
@@ -462,6 +476,8 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     extra = {"per_rank_gib_s": round(per_rank, 2), "fp32_allreduce_gib_s": round(fp32, 2),
              "ratio_vs_fp32": round(per_rank / fp32, 3), "fp32_ms_per_step": round(t_f * 1e3, 3),
              "pieces": args.pieces or "auto", "unpieced_ms_per_step": round(t_u * 1e3, 3),
+             "comm_only_ms": round(t_comm * 1e3, 3),
+             "comm_only_note": "RCCL alltoall + in-place allgather of the op's S compressed bytes, nothing else",
              "decentralized_bf16": decentralized,
              "onebit_allreduce": {"ms_per_step": round(t_o * 1e3, 3), "unpieced_ms_per_step": round(t_ou * 1e3, 3),
                                   "per_rank_gib_s": round(4.0 * n / t_o / GiB, 2),
