@@ -105,6 +105,73 @@ def centralized_pieced_rank(rank: int, world: int, port: int, inputs_path: str, 
         dist.destroy_process_group()
 
 
+def _onebit_piece_bytes(cs: int, co: int, pieces: int, q: int, header: bool) -> tuple[int, int]:
+    # comm_ops.cpp onebit_piece_bytes: tile range of bagua_onebit_piece_range, 128 B per tile
+    import ctypes
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = ctypes.CDLL(os.path.join(root, "bagua-core_amd", "lib", "libbagua_kernels.so"))
+    b, e = ctypes.c_int(), ctypes.c_int()
+    assert lib.bagua_onebit_piece_range(cs, pieces, q, ctypes.byref(b), ctypes.byref(e)) == 0
+    tiles = (cs + 1023) // 1024
+    lo = 0 if header else 32 + 128 * b.value
+    hi = co if e.value >= tiles else 32 + 128 * e.value
+    if not header and b.value >= e.value:
+        return 0, 0
+    return lo, hi
+
+
+def _alltoall_range(send: np.ndarray, recv: np.ndarray, p: int, co: int, lo: int, hi: int) -> None:
+    if hi <= lo:
+        return
+    part = torch.from_numpy(np.concatenate([send[j * co + lo:j * co + hi] for j in range(p)]))
+    got = torch.empty_like(part)
+    dist.all_to_all_single(got, part)
+    g = got.numpy()
+    for j in range(p):
+        recv[j * co + lo:j * co + hi] = g[j * (hi - lo):(j + 1) * (hi - lo)]
+
+
+def _allgather_range(send: np.ndarray, rank: int, p: int, co: int, lo: int, hi: int) -> None:
+    if hi <= lo:
+        return
+    got = torch.empty(p * (hi - lo), dtype=torch.uint8)
+    dist.all_gather_into_tensor(got, torch.from_numpy(send[rank * co + lo:rank * co + hi].copy()))
+    g = got.numpy()
+    for j in range(p):
+        send[j * co + lo:j * co + hi] = g[j * (hi - lo):(j + 1) * (hi - lo)]
+
+
+def centralized_onebit_pieced_rank(rank: int, world: int, port: int, inputs_path: str, out_dir: str, dtype: int,
+                                   pieces: int) -> None:
+    """The pipelined 1-bit op's exchange protocol (comm_ops.cpp centralized_pipelined_onebit):
+    sign bits piece by piece, headers after the last alltoall piece, headers with the first
+    allgather piece."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        with np.load(inputs_path, allow_pickle=False) as z:
+            t = z[f"x{rank}"].copy()
+        p = world
+        cs = t.size // p
+        send = C.compress_onebit(t, dtype, p, -1)
+        S = send.size
+        co = S // p
+        recv = np.full(S, 0xAB, np.uint8)  # poison: every byte must arrive through a piece
+        for q in range(pieces):
+            _alltoall_range(send, recv, p, co, *_onebit_piece_bytes(cs, co, pieces, q, False))
+        _alltoall_range(send, recv, p, co, 0, 32)
+        C.decompress_onebit(recv, p, t, dtype)
+        C.reduce_chunks(t, dtype, p, rank, True)
+        C.compress_onebit(t, dtype, p, rank, out=send)
+        for q in range(pieces):
+            _allgather_range(send, rank, p, co, *_onebit_piece_bytes(cs, co, pieces, q, q == 0))
+        C.decompress_onebit(send, p, t, dtype)
+        np.save(os.path.join(out_dir, f"out{rank}.npy"), t.view(np.uint8))
+    finally:
+        dist.destroy_process_group()
+
+
 def decentralized_rank(rank: int, world: int, port: int, inputs_path: str, out_dir: str, dtype: int) -> None:
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

@@ -58,6 +58,23 @@ def test_centralized_pieced_gloo(tmp_path, world, dtype, cs, pieces):
         assert np.array_equal(np.load(tmp_path / f"out{r}.npy"), want[r].view(np.uint8)), f"rank {r}"
 
 
+@pytest.mark.parametrize("world,dtype,cs,pieces", [(2, 0, 5000, 3), (4, 0, 1024 * 9 + 7, 4), (3, 2, 2048, 4)])
+def test_centralized_onebit_pieced_gloo(tmp_path, world, dtype, cs, pieces):
+    """The pipelined 1-bit op's per-piece byte ranges (real bagua_onebit_piece_range; headers
+    after the last alltoall piece, with the first allgather piece) moved between gloo
+    processes reproduce the reference op sequence with the 1-bit codec bit-for-bit."""
+    oracle_c.build()
+    rng = np.random.default_rng(world * 13 + dtype + pieces)
+    xs = [NP.from_f32((rng.standard_normal(world * cs) * 1e-3).astype(np.float32), dtype) for _ in range(world)]
+    inputs = tmp_path / "in.npz"
+    np.savez(inputs, **{f"x{r}": x for r, x in enumerate(xs)})
+    mp.spawn(dist_worker.centralized_onebit_pieced_rank, args=(world, _free_port(), str(inputs), str(tmp_path),
+                                                               dtype, pieces), nprocs=world, join=True)
+    want = simulate.centralized_low_precision(oracle_c, xs, dtype, True, method="OneBitSignScale")
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"out{r}.npy"), want[r].view(np.uint8)), f"rank {r}"
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_decentralized_ring_gloo(tmp_path, world):
     oracle_c.build()
