@@ -25,6 +25,7 @@ from __future__ import annotations
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import time
@@ -383,9 +384,20 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item()) / steps
 
+    side_errors = {}
+
+    def side(name, fn):
+        # side measurements must not cost the headline line: an error that every rank
+        # raises alike (argument checks, an unsupported shape) is recorded instead
+        try:
+            return timed(fn, max(3, args.steps // 2), max(1, args.warmup // 2))
+        except Exception as e:  # noqa: BLE001
+            side_errors[name] = str(e)[:200]
+            return float("nan")
+
     t_c = timed(compressed_step, args.steps, args.warmup)
-    t_u = timed(lambda: compressed_step(1), max(3, args.steps // 2), max(1, args.warmup // 2))
-    t_f = timed(fp32_step, max(3, args.steps // 2), max(1, args.warmup // 2))
+    t_u = side("unpieced", lambda: compressed_step(1))
+    t_f = side("fp32_allreduce", fp32_step)
     # the same all-reduce with the 1-bit sign+scale codec (this repo's extension:
     # N/8 wire bytes per phase instead of N), fused middle step
     def onebit_step(pieces=args.pieces):
@@ -404,10 +416,10 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         N.check(N.C.bagua_comm_allgather_inplace(comm.handle, ctypes.byref(craw[1])), "allgather")
         N.check(N.C.bagua_comm_synchronize(comm.handle), "sync")
 
-    t_comm = timed(comm_only, max(3, args.steps // 2), max(1, args.warmup // 2))
+    t_comm = side("comm_only", comm_only)
     del cbuf, craw
-    t_o = timed(onebit_step, max(3, args.steps // 2), max(1, args.warmup // 2))
-    t_ou = timed(lambda: onebit_step(1), max(3, args.steps // 2), max(1, args.warmup // 2))
+    t_o = side("onebit", onebit_step)
+    t_ou = side("onebit_unpieced", lambda: onebit_step(1))
     decentralized = None
     if not args.no_decentralized:
         # config 5: bf16 bucket, decentralized ring exchange with the uint8 codec
@@ -421,7 +433,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
                 N.check(N.C.bagua_decentralized_low_precision_synchronous(
                     comm.handle, *[ctypes.byref(r) for r in draws], N.COMPRESSION_MINMAX_UINT8), "decentralized")
 
-            t_d = timed(dec_step, max(3, args.steps // 2), max(1, args.warmup // 2))
+            t_d = side("decentralized", dec_step)
             decentralized = {"config_index": 5, "elements_per_rank": nb, "dtype": "bf16",
                              "ms_per_step": round(t_d * 1e3, 3),
                              "gib_s_per_rank": round(2.0 * nb / t_d / GiB, 2),
@@ -483,8 +495,21 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
                                   "per_rank_gib_s": round(4.0 * n / t_o / GiB, 2),
                                   "ratio_vs_fp32": round((4.0 * n / t_o) / (4.0 * n / t_f), 3)},
              "per_kernel_us": {nm: round(t * 1e3, 2) for nm, t in zip(names, per)}}
+    if side_errors:
+        extra["side_errors"] = side_errors
     del comm
     return value, t_c * 1e3, roof, cfg, extra
+
+
+def _finite(o):
+    """NaN / inf (a failed side measurement) -> null: the line stays strict JSON."""
+    if isinstance(o, float):
+        return o if math.isfinite(o) else None
+    if isinstance(o, dict):
+        return {k: _finite(v) for k, v in o.items()}
+    if isinstance(o, (list, tuple)):
+        return [_finite(v) for v in o]
+    return o
 
 
 def main():
@@ -522,7 +547,7 @@ def main():
                         ("in pinned host memory (H2D + D2H timed)" if workload == "host" else "resident in HBM"),
                 "config": cfg, "roofline": roof, "cpu_baseline": cpu}
         line.update(extra)
-        print(json.dumps(line), file=json_out, flush=True)
+        print(json.dumps(_finite(line)), file=json_out, flush=True)
     if world > 1:
         import torch.distributed as dist
         if dist.is_initialized():
