@@ -77,6 +77,7 @@ KERNEL_SIGNATURES = {
     "bagua_minmax_u8_requantize_pieces": (_i32, [_i32, _vp, _i32, _i32, _vp, _sz, _i32, _i32, _vp, _sz, _vp]),
     "bagua_ring_mix_minmax": (_i32, [_i32, _vp, _vp, _vp, _vp, _i32, _vp, _sz, _vp]),
     "bagua_ring_apply_minmax": (_i32, [_i32, _vp, _vp, _vp, _sz, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "bagua_ring_apply_minmax_range": (_i32, [_i32, _vp, _vp, _vp, _sz, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "bagua_onebit_compressed_bytes": (_sz, [_i32, _i32]),
     "bagua_onebit_workspace_bytes": (_sz, [_i32, _i32]),
     "bagua_onebit_compress": (_i32, [_i32, _vp, _i32, _i32, _i32, _vp, _sz, _vp, _sz, _i32, _vp]),
@@ -164,6 +165,7 @@ CORE_SIGNATURES = {
     "bagua_centralized_full_precision_synchronous": (_i32, [_C, _T, _i32]),
     "bagua_decentralized_low_precision_synchronous": (_i32, [_C, _T, _T, _T, _T, _i32]),
     "bagua_decentralized_low_precision_synchronous_unfused": (_i32, [_C, _T, _T, _T, _T, _i32]),
+    "bagua_decentralized_low_precision_pipelined": (_i32, [_C, _T, _T, _T, _T, _i32, _i32]),
 }
 
 K = type("K", (), {})()

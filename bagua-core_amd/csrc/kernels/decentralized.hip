@@ -95,7 +95,9 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
                                                             typename T::storage* __restrict__ t,
                                                             typename T::storage* __restrict__ w,
                                                             typename T::storage* __restrict__ l,
-                                                            typename T::storage* __restrict__ r, int64_t n) {
+                                                            typename T::storage* __restrict__ r, int64_t n,
+                                                            int64_t e0, int64_t e1) {
+    // elements [e0, e1) (e0 a multiple of N; e1 too unless it is n)
     constexpr int N = Vec<T>::N;
     const QParams qm = read_header<T>(mine), ql = read_header<T>(from_left), qr = read_header<T>(from_right);
     // per-byte dequantised values of the three buffers (codec_common.hpp "dequantisation tables")
@@ -108,9 +110,9 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
     const uint8_t* pm = mine + 32;
     const uint8_t* pl = from_left + 32;
     const uint8_t* pr = from_right + 32;
-    const int64_t nvec = n / N;
+    const int64_t nvec = n / N, v1 = e1 / N;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nvec; v += stride) {
+    for (int64_t v = e0 / N + (int64_t)blockIdx.x * kBlock + threadIdx.x; v < v1; v += stride) {
         uint32_t bm[N], bl[N], br[N];
         load_bytes<T>(pm + v * N, bm);
         load_bytes<T>(pl + v * N, bl);
@@ -134,7 +136,7 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
         nt_store16(ot, reinterpret_cast<uint4*>(t) + v);
         nt_store16(ot, reinterpret_cast<uint4*>(w) + v);         // W = t (clone)
     }
-    if (blockIdx.x == 0 && threadIdx.x < n - nvec * N) {
+    if (e1 == n && blockIdx.x == 0 && threadIdx.x < n - nvec * N) {
         const int64_t j = nvec * N + threadIdx.x;
         l[j] = T::from_f(T::to_f(l[j]) + tl[pl[j]]);
         r[j] = T::from_f(T::to_f(r[j]) + tr[pr[j]]);
@@ -173,19 +175,23 @@ static int mix_impl(void* t, const void* l, const void* r, const void* w, int n,
 
 template <typename T>
 static int apply_impl(const uint8_t* mine, const uint8_t* from_left, const uint8_t* from_right, size_t comp_bytes,
-                      int n, void* t, void* w, void* l, void* r, hipStream_t s) {
+                      int n, void* t, void* w, void* l, void* r, hipStream_t s, int e0 = 0, int e1 = -1) {
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
+    if (e1 < 0) e1 = n;
     if (!mine || !from_left || !from_right || !t || !w || !l || !r || n < 0) return BAGUA_ERR_INVALID_ARG;
+    if (e0 < 0 || e1 < e0 || e1 > n || e0 % N || (e1 != n && e1 % N)) return BAGUA_ERR_INVALID_ARG;
+    if (e1 == e0) return BAGUA_OK;
     if (comp_bytes < (size_t)n + 32) return BAGUA_ERR_INVALID_ARG;
     if (!aligned16(t) || !aligned16(w) || !aligned16(l) || !aligned16(r)) return BAGUA_ERR_UNSUPPORTED;
     for (const uint8_t* p : {mine, from_left, from_right})
         if ((uintptr_t)(p + 32) % N) return BAGUA_ERR_UNSUPPORTED;
-    int64_t blocks = ((int64_t)n / N + kBlock - 1) / kBlock;
+    int64_t blocks = ((int64_t)(e1 - e0) / N + kBlock - 1) / kBlock;
     if (blocks > 2 * kTargetBlocks) blocks = 2 * kTargetBlocks;
     if (blocks < 1) blocks = 1;
     launch(ring_apply_kernel<T>, dim3(blocks), dim3(kBlock), 0, s, mine, from_left, from_right,
-                       static_cast<S*>(t), static_cast<S*>(w), static_cast<S*>(l), static_cast<S*>(r), (int64_t)n);
+           static_cast<S*>(t), static_cast<S*>(w), static_cast<S*>(l), static_cast<S*>(r), (int64_t)n, (int64_t)e0,
+           (int64_t)e1);
     return check_launch();
 }
 
@@ -225,6 +231,24 @@ int bagua_ring_apply_minmax(int dtype, const uint8_t* mine, const uint8_t* from_
         case BAGUA_DTYPE_BF16:
             return apply_impl<BF16>(mine, from_left, from_right, compressed_bytes, num_elem, tensor, weight, left,
                                     right, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+int bagua_ring_apply_minmax_range(int dtype, const uint8_t* mine, const uint8_t* from_left, const uint8_t* from_right,
+                                  size_t compressed_bytes, int num_elem, int elem_begin, int elem_end, void* tensor,
+                                  void* weight, void* left, void* right, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return apply_impl<F32>(mine, from_left, from_right, compressed_bytes, num_elem, tensor, weight, left,
+                                   right, s, elem_begin, elem_end);
+        case BAGUA_DTYPE_F16:
+            return apply_impl<F16>(mine, from_left, from_right, compressed_bytes, num_elem, tensor, weight, left,
+                                   right, s, elem_begin, elem_end);
+        case BAGUA_DTYPE_BF16:
+            return apply_impl<BF16>(mine, from_left, from_right, compressed_bytes, num_elem, tensor, weight, left,
+                                    right, s, elem_begin, elem_end);
     }
     return BAGUA_ERR_UNSUPPORTED;
 }

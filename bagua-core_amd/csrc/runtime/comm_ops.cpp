@@ -391,8 +391,27 @@ int bagua_centralized_full_precision_synchronous(BaguaSingleCommunicatorC* c, co
     return finish(c, rc);
 }
 
+// piece q of the ring exchange: bytes [lo, hi) of the whole-bucket segment to and
+// from both ring peers, one group on the side stream
+static int ring_exchange_range(BaguaSingleCommunicatorC* c, uint8_t* mine, uint8_t* lbuf, uint8_t* rbuf, size_t lo,
+                               size_t hi) {
+    if (hi <= lo) return BAGUA_OK;
+    const int p = (int)c->nranks, r = (int)c->rank;
+    const int lpeer = (r + p - 1) % p, rpeer = (r + 1) % p;
+    const size_t len = hi - lo;
+    hipStream_t s1 = c->side;
+    int rc = c->t->group_start();
+    if (!rc) rc = c->t->send(mine + lo, len, BAGUA_DTYPE_U8, lpeer, s1);
+    if (!rc) rc = c->t->send(mine + lo, len, BAGUA_DTYPE_U8, rpeer, s1);
+    if (!rc) rc = c->t->recv(lbuf + lo, len, BAGUA_DTYPE_U8, lpeer, s1);
+    if (!rc) rc = c->t->recv(rbuf + lo, len, BAGUA_DTYPE_U8, rpeer, s1);
+    const int rc_end = c->t->group_end();
+    return rc ? rc : rc_end;
+}
+
 static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, const bagua_tensor_t* weight,
-                         const bagua_tensor_t* left, const bagua_tensor_t* right, int method, bool allow_fused) {
+                         const bagua_tensor_t* left, const bagua_tensor_t* right, int method, bool allow_fused,
+                         int pieces = 1) {
     if (!c || !c->t || !t || !weight || !left || !right) return BAGUA_ERR_INVALID_ARG;
     if (c->aborted.load()) return BAGUA_ERR_ABORTED;
     DeviceGuard guard(c->device_id);
@@ -427,6 +446,47 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
         if (!ws) return finish(c, BAGUA_ERR_OOM);
         rc = bagua_ring_mix_minmax(t->dtype, tp, lp, rp, wp, n, ws, wsb, sp);
         if (rc == BAGUA_OK) {
+            if (pieces < 1) pieces = c->nranks == 1 ? 1 : auto_pieces((size_t)n);
+            if (pieces > 1) {
+                // pipelined: quantise piece q -> exchange piece q (side stream) -> apply piece q;
+                // one header for the whole bucket, travelling with piece 0
+                Chunking k;
+                k.p = 1;
+                k.cs = (size_t)n;
+                k.S = S;
+                if (c->ensure_side(2 * (size_t)pieces + 1)) return finish(c, BAGUA_ERR_HIP);
+                hipStream_t s1 = c->side;
+                hipEvent_t* quantised = c->events.data();
+                hipEvent_t* exchanged = quantised + pieces;
+                hipEvent_t start = exchanged[pieces];
+                uint8_t* mb = mine.as<uint8_t>();
+                uint8_t* lb = lbuf.as<uint8_t>();
+                uint8_t* rb = rbuf.as<uint8_t>();
+                HIP2(hipEventRecord(start, c->stream));
+                HIP2(hipStreamWaitEvent(s1, start, 0));
+                for (int q = 0; q < pieces; ++q) {
+                    int b, e;
+                    bagua_minmax_u8_piece_range(n, pieces, q, &b, &e);
+                    if (q == 0 || b < e)
+                        TRY2(bagua_minmax_u8_quantize_range(t->dtype, tp, n, n, 1, mb, S, ws, wsb, -1, b, e, sp));
+                    HIP2(hipEventRecord(quantised[q], c->stream));
+                }
+                for (int q = 0; q < pieces; ++q) {
+                    size_t lo, hi;
+                    piece_bytes(k, pieces, q, &lo, &hi);
+                    HIP2(hipStreamWaitEvent(s1, quantised[q], 0));
+                    TRY2(ring_exchange_range(c, mb, lb, rb, lo, hi));
+                    HIP2(hipEventRecord(exchanged[q], s1));
+                }
+                for (int q = 0; q < pieces; ++q) {
+                    int b, e;
+                    bagua_minmax_u8_piece_range(n, pieces, q, &b, &e);
+                    HIP2(hipStreamWaitEvent(c->stream, exchanged[q], 0));
+                    if (b < e)
+                        TRY2(bagua_ring_apply_minmax_range(t->dtype, mb, lb, rb, S, n, b, e, tp, wp, lp, rp, sp));
+                }
+                return finish_both(c, BAGUA_OK);
+            }
             TRY(bagua_minmax_u8_compress_stage(2, t->dtype, tp, n, n, 1, mine.as<uint8_t>(), S, ws, wsb, -1, sp));
             mixed = true;
         } else if (rc != BAGUA_ERR_UNSUPPORTED) {
@@ -471,7 +531,13 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
 int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t,
                                                   const bagua_tensor_t* weight, const bagua_tensor_t* left,
                                                   const bagua_tensor_t* right, int method) {
-    return decentralized(c, t, weight, left, right, method, true);
+    return decentralized(c, t, weight, left, right, method, true, 0);
+}
+
+int bagua_decentralized_low_precision_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t,
+                                                const bagua_tensor_t* weight, const bagua_tensor_t* left,
+                                                const bagua_tensor_t* right, int method, int pieces) {
+    return decentralized(c, t, weight, left, right, method, true, pieces);
 }
 
 int bagua_decentralized_low_precision_synchronous_unfused(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t,

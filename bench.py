@@ -429,13 +429,15 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             bufs = [(torch.randn(nb, device=dev, generator=g) * 1e-3).to(torch.bfloat16) for _ in range(4)]
             draws = [BaguaTensorPy(b, k).raw() for b, k in zip(bufs, "twlr")]
 
-            def dec_step():
-                N.check(N.C.bagua_decentralized_low_precision_synchronous(
-                    comm.handle, *[ctypes.byref(r) for r in draws], N.COMPRESSION_MINMAX_UINT8), "decentralized")
+            def dec_step(pieces=args.pieces):
+                N.check(N.C.bagua_decentralized_low_precision_pipelined(
+                    comm.handle, *[ctypes.byref(r) for r in draws], N.COMPRESSION_MINMAX_UINT8, pieces),
+                    "decentralized")
 
             t_d = side("decentralized", dec_step)
+            t_du = side("decentralized_unpieced", lambda: dec_step(1))
             decentralized = {"config_index": 5, "elements_per_rank": nb, "dtype": "bf16",
-                             "ms_per_step": round(t_d * 1e3, 3),
+                             "ms_per_step": round(t_d * 1e3, 3), "unpieced_ms_per_step": round(t_du * 1e3, 3),
                              "gib_s_per_rank": round(2.0 * nb / t_d / GiB, 2),
                              "gib_s_total": round(world * 2.0 * nb / t_d / GiB, 2)}
             del bufs, draws

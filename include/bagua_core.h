@@ -128,9 +128,10 @@ int bagua_centralized_low_precision_synchronous(BaguaSingleCommunicatorC* comm, 
 /* The same op with each chunk cut into `pieces` element ranges, the exchange of
  * one piece (side stream, grouped send/recv) overlapping the codec kernels of
  * the next; bit-identical to the unpieced op.  pieces = 0 picks automatically
- * (BAGUA_PIPELINE_PIECES cap, default 4; BAGUA_PIPELINE_MIN_PIECE elements per
- * piece, default 1 Mi), 1 disables; the op above runs this with pieces = 0.
- * MinMaxUInt8 only; shapes the fused kernels cannot take run unpieced. */
+ * (BAGUA_PIPELINE_PIECES cap, default 4; BAGUA_PIPELINE_MIN_PIECE payload bytes
+ * per chunk piece, default 1 MiB; one rank: unpieced), 1 disables; the op above
+ * runs this with pieces = 0.  MinMaxUInt8 and the 1-bit codec; shapes the fused
+ * kernels cannot take run unpieced. */
 int bagua_centralized_low_precision_pipelined(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t, int average,
                                               int method, int pieces);
 /* the reference's unfused sequence, kept for A/B measurement and parity */
@@ -144,6 +145,14 @@ int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* comm
                                                   const bagua_tensor_t* weight,
                                                   const bagua_tensor_t* left_peer_weight,
                                                   const bagua_tensor_t* right_peer_weight, int method);
+/* The same with the bucket cut into `pieces` element ranges: after the mix pass
+ * (whole-bucket min/max), piece q is quantised, sent to both peers on a side
+ * stream and applied as it arrives, so quantise, exchange and apply overlap;
+ * bit-identical to the unpieced op.  pieces = 0 picks automatically (as above),
+ * 1 disables; the op above runs this with pieces = 0. */
+int bagua_decentralized_low_precision_pipelined(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,
+                                                const bagua_tensor_t* weight, const bagua_tensor_t* left_peer_weight,
+                                                const bagua_tensor_t* right_peer_weight, int method, int pieces);
 /* the reference's unfused op sequence (3 addmul, compress, 3 x decompress + add, clone), for A/B */
 int bagua_decentralized_low_precision_synchronous_unfused(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,
                                                           const bagua_tensor_t* weight,

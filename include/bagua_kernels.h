@@ -199,6 +199,12 @@ int bagua_ring_mix_minmax(int dtype, void* tensor, const void* left, const void*
 int bagua_ring_apply_minmax(int dtype, const uint8_t* mine, const uint8_t* from_left, const uint8_t* from_right,
                             size_t compressed_bytes, int num_elem, void* tensor, void* weight, void* left,
                             void* right, bagua_stream_t stream);
+/* The same on elements [elem_begin, elem_end) only (the pipelined op applies each
+ * piece as it arrives; elem_begin and elem_end multiples of 16 / sizeof(T), or
+ * elem_end = num_elem; the headers of all three buffers must be present). */
+int bagua_ring_apply_minmax_range(int dtype, const uint8_t* mine, const uint8_t* from_left, const uint8_t* from_right,
+                                  size_t compressed_bytes, int num_elem, int elem_begin, int elem_end, void* tensor,
+                                  void* weight, void* left, void* right, bagua_stream_t stream);
 
 /* K:196-266 elementwise kernels, dtype-generic (f32, f16, bf16) */
 int bagua_add_inplace(int dtype, void* x, const void* y, int n, bagua_stream_t stream);

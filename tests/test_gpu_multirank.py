@@ -226,3 +226,32 @@ def test_decentralized_low_precision_multirank(bc, oracle_c, p, dtype, n, unfuse
     for k, wk in zip("twlr", want):
         for r in range(p):
             assert np.array_equal(host(dts[k][r], dtype).view(np.uint8), wk[r].view(np.uint8)), f"{k} rank {r}"
+
+
+@pytest.mark.parametrize("p,dtype,n,pieces", [(2, F32, 30011, 3), (3, BF16, 70001, 4), (4, F16, 65536 + 7, 2),
+                                             (8, F32, 30011, 5), (1, BF16, 40000, 3), (2, BF16, (1 << 21) + 3, 0),
+                                             (3, F32, 1000, 4)])
+def test_decentralized_pipelined_multirank(bc, oracle_c, p, dtype, n, pieces):
+    """Pieced ring op (quantise piece q -> send/recv piece q on the side stream -> apply piece q;
+    one header travelling with piece 0) == the oracle's op simulation, all four tensors.
+    (3, F32, 1000, 4): a single 512-aligned piece plus empty ones; pieces = 0: automatic."""
+    from bagua_core.communicator import loopback_communicators
+    rng = np.random.default_rng(900 + p + n + pieces)
+    arrs = {k: [NP.from_f32((rng.standard_normal(n) * 1e-3).astype(np.float32), dtype) for _ in range(p)]
+            for k in "twlr"}
+    want = simulate.decentralized_low_precision(oracle_c, arrs["t"], arrs["w"], arrs["l"], arrs["r"], dtype)
+    comms = loopback_communicators(p, 0)
+    dts = {k: [dev(a, dtype) for a in arrs[k]] for k in "twlr"}
+    torch.cuda.synchronize()
+    N = bc._native
+
+    def rank(r):
+        raws = [bc.BaguaTensorPy(dts[k][r], k).raw() for k in "twlr"]
+        N.check(N.C.bagua_decentralized_low_precision_pipelined(comms[r].handle, *[ctypes.byref(x) for x in raws],
+                                                                N.COMPRESSION_MINMAX_UINT8, pieces), f"rank {r}")
+
+    run_ranks(rank, p)
+    for k, wk in zip("twlr", want):
+        for r in range(p):
+            assert np.array_equal(host(dts[k][r], dtype).view(np.uint8), wk[r].view(np.uint8)), f"{k} rank {r}"
+
