@@ -543,7 +543,10 @@ static ResidentPlan resident_plan(const void* input, int64_t in_num_elem, int64_
     const int64_t chunk_offset = out_bytes / p;
     // whole chunks only, every active chunk fully valid, large enough to pay for the exchange
     if (in_num_elem < (target < 0 ? (int64_t)p * cs : ((int64_t)target + 1) * cs)) return pl;
-    if (cs * nact < env_int("BAGUA_RESIDENT_MIN_ELEMS", 1 << 22)) return pl;
+    // below ~12 Mi elements the fixed cost of the exchange (~4 us: publish + sweep across
+    // XCDs) and of starting one 512-thread workgroup per CU (~3 us) loses to the
+    // two-kernel encode (crossover between 8 Mi and 16 Mi)
+    if (cs * nact < env_int("BAGUA_RESIDENT_MIN_ELEMS", 12 << 20)) return pl;
     for (int i = 0; i < nact; ++i) {
         const int c = target < 0 ? i : target;
         const uintptr_t src = (uintptr_t)(static_cast<const S*>(input) + (int64_t)c * cs);

@@ -1,7 +1,8 @@
 """GPU parity of the one-launch MinMax-UInt8 encode (minmax_resident.hip).
 
 bagua_minmax_u8_compress takes this path for whole, fully valid chunks of
->= 4 Mi elements in total; every case here first asserts that it does
+>= 12 Mi elements in total (BAGUA_RESIDENT_MIN_ELEMS; lowered to 4 Mi here so
+the cases stay small); every case here first asserts that it does
 (bagua_minmax_u8_resident_path), then compares every byte of the compressed
 buffer with the C oracle (the reference's compress, K:533-571).  Covered:
 every dtype, p = 1 / 3 (idle workgroups: the CU count is not a multiple of
@@ -39,6 +40,17 @@ def env():
             os.environ.pop(k, None)
         else:
             os.environ[k] = v
+
+
+@pytest.fixture(autouse=True)
+def small_threshold():
+    old = os.environ.get("BAGUA_RESIDENT_MIN_ELEMS")
+    os.environ["BAGUA_RESIDENT_MIN_ELEMS"] = str(1 << 22)
+    yield
+    if old is None:
+        os.environ.pop("BAGUA_RESIDENT_MIN_ELEMS", None)
+    else:
+        os.environ["BAGUA_RESIDENT_MIN_ELEMS"] = old
 
 
 def make_input(n: int, dtype: int, seed: int, specials: bool = False) -> np.ndarray:
@@ -164,3 +176,16 @@ def test_resident_decode_round_trip_256mib(K, oracle_c):
     dw = np.empty_like(xh)
     oracle_c.decompress_minmax_u8(want, 1, dw, F32)
     assert np.array_equal(y.cpu().numpy().view(np.uint32), dw.view(np.uint32))
+
+
+def test_default_size_threshold(K):
+    """Default: the two-kernel encode below 12 Mi elements (it is faster there), the
+    one-launch encode from 12 Mi on."""
+    os.environ.pop("BAGUA_RESIDENT_MIN_ELEMS", None)
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    xt = torch.empty(16 << 20, device="cuda")
+    for n, want in ((8 << 20, 0), ((12 << 20) - 1024, 0), (12 << 20, 1), (16 << 20, 1)):
+        S = K.bagua_minmax_u8_compressed_bytes(F32, n, 1)
+        out = torch.empty(S, dtype=torch.uint8, device="cuda")
+        assert K.bagua_minmax_u8_resident_path(F32, xt.data_ptr(), n, n, 1, out.data_ptr(), S, -1, sp) == want, n
+
