@@ -334,6 +334,14 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
         __hip_atomic_store(mine + 1, ((uint64_t)tag << 32) | hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
+    // the first tile pass 2 re-reads (the top full tile: reverse order) is loaded
+    // now, so its latency overlaps the exchange wait instead of following it
+    const int64_t tile2 = (int64_t)SB * BLOCK;
+    const int64_t nfull2 = v1 > stream0 ? (v1 - stream0) / tile2 : 0;
+    uint4 pre[SB], pre2[SB];
+    if (nfull2 > 0) load_tile<SB, BLOCK, NT>(v, stream0 + (nfull2 - 1) * tile2, t, pre);
+    if (nfull2 > 1) load_tile<SB, BLOCK, NT>(v, stream0 + (nfull2 - 2) * tile2, t, pre2);
+
     trace_stamp(a, g, 1);
     // ---- exchange ------------------------------------------------------------
     if (w == 0) {
@@ -381,9 +389,10 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
         }
         if (nfull > 0) {
             uint4 ra[SB], rb[SB];
-            load_tile<SB, BLOCK, NT>(v, stream0 + (nfull - 1) * tile, t, ra);
+#pragma unroll
+            for (int j = 0; j < SB; ++j) { ra[j] = pre[j]; rb[j] = pre2[j]; }  // loaded before the exchange
             for (int64_t i = nfull - 1; i >= 0; i -= 2) {
-                load_tile<SB, BLOCK, NT>(v, stream0 + (i >= 1 ? i - 1 : 0) * tile, t, rb);
+                if (i != nfull - 1 || nfull < 2) load_tile<SB, BLOCK, NT>(v, stream0 + (i >= 1 ? i - 1 : 0) * tile, t, rb);
                 const int64_t ba = stream0 + i * tile;
 #pragma unroll
                 for (int j = 0; j < SB; ++j) quant_store<T>(ra[j], q, vdst + (ba + j * BLOCK + t) * N);
