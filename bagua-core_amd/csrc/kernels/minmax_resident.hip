@@ -406,16 +406,37 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
         }
     }
     trace_stamp(a, g, 4);
+    if (v0 + (int64_t)(R + H) * BLOCK <= v1) {
+        // the whole on-chip part is inside the slice (every slice of a bucket this path
+        // takes): no per-vector guards, so the LDS reads of a batch issue back to back
+        // and the quantise+stores pipeline (a guarded vector was its own exec-masked
+        // block that waited on its own ds_read: 11 us for 36 % of the payload)
+        uint8_t* vd = vdst + (v0 + t) * N;
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-        const int64_t i = v0 + (int64_t)(R + k) * BLOCK + t;
-        if (i < v1) quant_store<T>(park[k * BLOCK + t], q, vdst + i * N);
-    }
-    trace_stamp(a, g, 5);
+        for (int kb = 0; kb < H; kb += SB) {
+            uint4 r[SB];
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-        const int64_t i = v0 + (int64_t)k * BLOCK + t;
-        if (i < v1) quant_store<T>(held[k], q, vdst + i * N);
+            for (int j = 0; j < SB; ++j)
+                if (kb + j < H) r[j] = park[(kb + j) * BLOCK + t];
+#pragma unroll
+            for (int j = 0; j < SB; ++j)
+                if (kb + j < H) quant_store<T>(r[j], q, vd + (int64_t)(R + kb + j) * BLOCK * N);
+        }
+        trace_stamp(a, g, 5);
+#pragma unroll
+        for (int k = 0; k < R; ++k) quant_store<T>(held[k], q, vd + (int64_t)k * BLOCK * N);
+    } else {
+#pragma unroll
+        for (int k = 0; k < H; ++k) {
+            const int64_t i = v0 + (int64_t)(R + k) * BLOCK + t;
+            if (i < v1) quant_store<T>(park[k * BLOCK + t], q, vdst + i * N);
+        }
+        trace_stamp(a, g, 5);
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t i = v0 + (int64_t)k * BLOCK + t;
+            if (i < v1) quant_store<T>(held[k], q, vdst + i * N);
+        }
     }
     if (a.trace != nullptr) {
         __syncthreads();
