@@ -255,3 +255,58 @@ def test_decentralized_pipelined_multirank(bc, oracle_c, p, dtype, n, pieces):
         for r in range(p):
             assert np.array_equal(host(dts[k][r], dtype).view(np.uint8), wk[r].view(np.uint8)), f"{k} rank {r}"
 
+
+def test_pipelined_ops_back_to_back_fuzz(bc, oracle_c):
+    """Random shapes, rank counts and piece counts, every pipelined op run twice in a row on
+    the same loopback communicators (pool buffers, events and workspaces are reused across
+    ops): each result equals the oracle's simulation of the reference op sequence."""
+    from bagua_core.communicator import loopback_communicators
+    rng = np.random.default_rng(4242)
+    N = bc._native
+    for case in range(6):
+        p = int(rng.integers(2, 9))
+        dtype = int(rng.choice([F32, F16, BF16]))
+        pieces = int(rng.integers(0, 6))
+        comms = loopback_communicators(p, 0)
+        # centralized MinMax and 1-bit (chunk sizes keep S % p == 0 for MinMax: multiples of 32)
+        cs = int(rng.integers(1, 40)) * 1024 + 32 * int(rng.integers(0, 8))
+        for method, name in ((N.COMPRESSION_MINMAX_UINT8, "MinMaxUInt8"), (N.COMPRESSION_ONEBIT, "OneBitSignScale")):
+            if method == N.COMPRESSION_MINMAX_UINT8 and oracle_c.minmax_compressed_size(p, cs, dtype) % p:
+                continue
+            xs = [NP.from_f32((rng.standard_normal(p * cs) * 1e-3).astype(np.float32), dtype) for _ in range(p)]
+            want = simulate.centralized_low_precision(oracle_c, xs, dtype, True, method=name)
+            want2 = simulate.centralized_low_precision(oracle_c, want, dtype, True, method=name)
+            ts = [dev(x, dtype) for x in xs]
+            torch.cuda.synchronize()
+
+            def rank(r, ts=ts, method=method):
+                raw = bc.BaguaTensorPy(ts[r], "g").raw()
+                for _ in range(2):
+                    N.check(N.C.bagua_centralized_low_precision_pipelined(comms[r].handle, ctypes.byref(raw), 1,
+                                                                          method, pieces), f"rank {r}")
+
+            run_ranks(rank, p)
+            for r in range(p):
+                assert np.array_equal(host(ts[r], dtype).view(np.uint8), want2[r].view(np.uint8)), \
+                    f"case {case} {name} p={p} cs={cs} pieces={pieces} rank {r}"
+        # decentralized ring
+        n = int(rng.integers(1, 300)) * 512 + int(rng.integers(0, 512))
+        arrs = {k: [NP.from_f32((rng.standard_normal(n) * 1e-3).astype(np.float32), dtype) for _ in range(p)]
+                for k in "twlr"}
+        w1 = simulate.decentralized_low_precision(oracle_c, arrs["t"], arrs["w"], arrs["l"], arrs["r"], dtype)
+        w2 = simulate.decentralized_low_precision(oracle_c, *w1, dtype)
+        dts = {k: [dev(a, dtype) for a in arrs[k]] for k in "twlr"}
+        torch.cuda.synchronize()
+
+        def drank(r):
+            raws = [bc.BaguaTensorPy(dts[k][r], k).raw() for k in "twlr"]
+            for _ in range(2):
+                N.check(N.C.bagua_decentralized_low_precision_pipelined(
+                    comms[r].handle, *[ctypes.byref(x) for x in raws], N.COMPRESSION_MINMAX_UINT8, pieces), f"rank {r}")
+
+        run_ranks(drank, p)
+        for k, wk in zip("twlr", w2):
+            for r in range(p):
+                assert np.array_equal(host(dts[k][r], dtype).view(np.uint8), wk[r].view(np.uint8)), \
+                    f"case {case} ring p={p} n={n} pieces={pieces} {k} rank {r}"
+
