@@ -275,25 +275,36 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
             const int64_t i = v0 + (int64_t)k * BLOCK + t;
             held[k] = v[i < vl ? i : vl];
         }
+        // software-pipelined: the next batch of parked vectors is in flight while the
+        // current one (first: the held vectors) is folded, so memory never waits on VALU
+        uint4 cur[SB], nxt[SB];
+#pragma unroll
+        for (int j = 0; j < SB; ++j) {
+            if (j < H) {
+                const int64_t i = v0 + (int64_t)(R + j) * BLOCK + t;
+                cur[j] = v[i < vl ? i : vl];
+            }
+        }
 #pragma unroll
         for (int k = 0; k < R; ++k) fold_vec<T>(held[k], lo, hi);
 #pragma unroll
         for (int kb = 0; kb < H; kb += SB) {
-            uint4 r[SB];
 #pragma unroll
             for (int j = 0; j < SB; ++j) {
-                if (kb + j < H) {
-                    const int64_t i = v0 + (int64_t)(R + kb + j) * BLOCK + t;
-                    r[j] = v[i < vl ? i : vl];
+                if (kb + SB + j < H) {
+                    const int64_t i = v0 + (int64_t)(R + kb + SB + j) * BLOCK + t;
+                    nxt[j] = v[i < vl ? i : vl];
                 }
             }
 #pragma unroll
             for (int j = 0; j < SB; ++j) {
                 if (kb + j < H) {
-                    fold_vec<T>(r[j], lo, hi);
-                    park[(kb + j) * BLOCK + t] = r[j];
+                    fold_vec<T>(cur[j], lo, hi);
+                    park[(kb + j) * BLOCK + t] = cur[j];
                 }
             }
+#pragma unroll
+            for (int j = 0; j < SB; ++j) cur[j] = nxt[j];
         }
         // streamed part: full tiles double-buffered (2 x SB loads in flight per
         // lane: with one wave per SIMD nothing else hides the latency), then the
