@@ -118,6 +118,26 @@ __device__ __forceinline__ uint32_t quant(float x, const QParams& q) {
     return (uint32_t)v;
 }
 
+// The level quant() converts, before the conversion: always an integer, NaN or
+// +-inf (rint results and lower_bound = ub - 255 are integers, so is their
+// difference after rounding).
+__device__ __forceinline__ float quant_level(float x, const QParams& q) {
+    const float level = __builtin_fminf(__builtin_rintf(x * q.scale), q.upper_bound);
+    return level - q.lower_bound;
+}
+
+// 4 quantised bytes packed LSB-first by v_cvt_pk_u8_f32, which converts AND places
+// a byte in one instruction.  On integers, NaN and +-inf -- every value
+// quant_level() produces -- it equals quant()'s saturating conversion
+// (tools/cvt_probe.hip checks all such f32 bit patterns: 0 mismatches; on
+// non-integers it rounds where the cast truncates, which cannot occur here).
+__device__ __forceinline__ uint32_t quant_pack4(float a, float b, float c, float d, const QParams& q) {
+    uint32_t w = __builtin_amdgcn_cvt_pk_u8_f32(quant_level(a, q), 0, 0u);
+    w = __builtin_amdgcn_cvt_pk_u8_f32(quant_level(b, q), 1, w);
+    w = __builtin_amdgcn_cvt_pk_u8_f32(quant_level(c, q), 2, w);
+    return __builtin_amdgcn_cvt_pk_u8_f32(quant_level(d, q), 3, w);
+}
+
 // K:424-432
 __device__ __forceinline__ float dequant(uint32_t b, const QParams& q) {
     return ((float)b + q.lower_bound) / q.scale;
@@ -232,6 +252,20 @@ __device__ __forceinline__ void store_bytes(uint8_t* p, uint32_t (&b)[Vec<T>::N]
         uint2 v;
         v.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
         v.y = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
+        *reinterpret_cast<uint2*>(p) = v;
+    }
+}
+
+// the N quantised bytes of one unpacked vector, as one 4-B (f32) / 8-B (16-bit)
+// plain store (see store_bytes for the cache policy)
+template <typename T>
+__device__ __forceinline__ void quant_store_vec(const float (&f)[Vec<T>::N], const QParams& q, uint8_t* p) {
+    if constexpr (Vec<T>::N == 4) {
+        *reinterpret_cast<uint32_t*>(p) = quant_pack4(f[0], f[1], f[2], f[3], q);
+    } else {
+        uint2 v;
+        v.x = quant_pack4(f[0], f[1], f[2], f[3], q);
+        v.y = quant_pack4(f[4], f[5], f[6], f[7], q);
         *reinterpret_cast<uint2*>(p) = v;
     }
 }

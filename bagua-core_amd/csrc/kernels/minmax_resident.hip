@@ -156,10 +156,7 @@ template <typename T>
 __device__ __forceinline__ void quant_store(const uint4& r, const QParams& q, uint8_t* dst) {
     float f[Vec<T>::N];
     unpack16<T>(r, f);
-    uint32_t bts[Vec<T>::N];
-#pragma unroll
-    for (int i = 0; i < Vec<T>::N; ++i) bts[i] = quant(f[i], q);
-    store_bytes<T>(dst, bts);
+    quant_store_vec<T>(f, q, dst);
 }
 
 // header of chunk c (slice 0), slack after the payload and the buffer tail

@@ -197,10 +197,7 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
                 const int64_t v = base + k * kBlock + threadIdx.x;
                 float f[N];
                 unpack16<T>(r[k], f);
-                uint32_t b[N];
-#pragma unroll
-                for (int i = 0; i < N; ++i) b[i] = quant(f[i], q);
-                store_bytes<T>(vdst + v * N, b);
+                quant_store_vec<T>(f, q, vdst + v * N);
             }
             continue;
         }
