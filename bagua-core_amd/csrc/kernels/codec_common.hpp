@@ -131,11 +131,16 @@ __device__ __forceinline__ float quant_level(float x, const QParams& q) {
 // quant_level() produces -- it equals quant()'s saturating conversion
 // (tools/cvt_probe.hip checks all such f32 bit patterns: 0 mismatches; on
 // non-integers it rounds where the cast truncates, which cannot occur here).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t quant_pack4(float a, float b, float c, float d, const QParams& q) {
-    uint32_t w = __builtin_amdgcn_cvt_pk_u8_f32(quant_level(a, q), 0, 0u);
-    w = __builtin_amdgcn_cvt_pk_u8_f32(quant_level(b, q), 1, w);
-    w = __builtin_amdgcn_cvt_pk_u8_f32(quant_level(c, q), 2, w);
-    return __builtin_amdgcn_cvt_pk_u8_f32(quant_level(d, q), 3, w);
+    // the products as two packed multiplies (v_pk_mul_f32: two IEEE products per lane)
+    const f32x2 s2 = {q.scale, q.scale};
+    const f32x2 p01 = f32x2{a, b} * s2, p23 = f32x2{c, d} * s2;
+    const float ub = q.upper_bound, lb = q.lower_bound;
+    uint32_t w = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(__builtin_rintf(p01.x), ub) - lb, 0, 0u);
+    w = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(__builtin_rintf(p01.y), ub) - lb, 1, w);
+    w = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(__builtin_rintf(p23.x), ub) - lb, 2, w);
+    return __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(__builtin_rintf(p23.y), ub) - lb, 3, w);
 }
 
 // K:424-432
