@@ -23,6 +23,13 @@ namespace bagua {
 
 int minmax_partials_blocks(int64_t cs, int per_vec, int nact, size_t ws_bytes);  // minmax_u8.hip
 
+// vectors per tensor per iteration, all loads issued before any is consumed
+// (profiles/r01_ring_unroll_ab.jsonl, 2^27 bf16, interleaved runs on one box:
+// apply 455-487 -> 406-436 us and the op 1.02-1.05 -> 0.97-1.01 ms from U = 1 to
+// U = 4; the mix moves within noise)
+constexpr int kMixUnroll = 4;
+constexpr int kApplyUnroll = 4;
+
 // K:236-244 addmul as the elementwise kernels compute it (elementwise.hip)
 template <typename T>
 __device__ __forceinline__ float addmul(float x, float y, float f) {
@@ -37,7 +44,7 @@ __device__ __forceinline__ float mix(float t, float l, float r, float w, float f
     return as_stored<T>(addmul<T>(t, w, f53));
 }
 
-template <typename T>
+template <typename T, int U>
 __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* __restrict__ t,
                                                           const typename T::storage* __restrict__ l,
                                                           const typename T::storage* __restrict__ r,
@@ -47,11 +54,8 @@ __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* _
     uint32_t lo = min_space(T::init_max()), hi = max_space(-T::init_max());
     const int64_t nvec = n / N;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nvec; v += stride) {
-        const uint4 rt = reinterpret_cast<const uint4*>(t)[v];
-        const uint4 rl = nt_load16(reinterpret_cast<const uint4*>(l) + v);
-        const uint4 rr = nt_load16(reinterpret_cast<const uint4*>(r) + v);
-        const uint4 rw = reinterpret_cast<const uint4*>(w)[v];
+    // one vector of each of the four tensors
+    auto body = [&](int64_t v, const uint4& rt, const uint4& rl, const uint4& rr, const uint4& rw) {
         float ft[N], fl[N], fr[N], fw[N];
         unpack16<T>(rt, ft);
         unpack16<T>(rl, fl);
@@ -66,6 +70,28 @@ __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* _
         }
         // plain store: the quantise pass re-reads t next
         reinterpret_cast<uint4*>(t)[v] = pack16<T>(ft);
+    };
+    const uint4* t4 = reinterpret_cast<const uint4*>(t);
+    const uint4* l4 = reinterpret_cast<const uint4*>(l);
+    const uint4* r4 = reinterpret_cast<const uint4*>(r);
+    const uint4* w4 = reinterpret_cast<const uint4*>(w);
+    // U vectors per tensor per iteration (4U x 16 B in flight per lane), all loads
+    // issued before any is consumed; the last partial iteration goes one by one
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nvec; v += stride * U) {
+        if (v + (U - 1) * stride < nvec) {
+            uint4 rt[U], rl[U], rr[U], rw[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                rt[k] = t4[v + k * stride];
+                rl[k] = nt_load16(l4 + v + k * stride);
+                rr[k] = nt_load16(r4 + v + k * stride);
+                rw[k] = w4[v + k * stride];
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) body(v + k * stride, rt[k], rl[k], rr[k], rw[k]);
+        } else {
+            for (int64_t u = v; u < nvec; u += stride) body(u, t4[u], nt_load16(l4 + u), nt_load16(r4 + u), w4[u]);
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x < n - nvec * N) {  // ragged tail
         const int64_t j = nvec * N + threadIdx.x;
@@ -88,7 +114,7 @@ __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* _
     }
 }
 
-template <typename T>
+template <typename T, int U>
 __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __restrict__ mine,
                                                             const uint8_t* __restrict__ from_left,
                                                             const uint8_t* __restrict__ from_right,
@@ -112,14 +138,8 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
     const uint8_t* pr = from_right + 32;
     const int64_t nvec = n / N, v1 = e1 / N;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t v = e0 / N + (int64_t)blockIdx.x * kBlock + threadIdx.x; v < v1; v += stride) {
-        uint32_t bm[N], bl[N], br[N];
-        load_bytes<T>(pm + v * N, bm);
-        load_bytes<T>(pl + v * N, bl);
-        load_bytes<T>(pr + v * N, br);
-        const uint4 rl = reinterpret_cast<const uint4*>(l)[v];
-        const uint4 rr = reinterpret_cast<const uint4*>(r)[v];
-        const uint4 rw = reinterpret_cast<const uint4*>(w)[v];
+    auto body = [&](int64_t v, const uint32_t (&bm)[N], const uint32_t (&bl)[N], const uint32_t (&br)[N],
+                    const uint4& rl, const uint4& rr, const uint4& rw) {
         float fl[N], fr[N], fw[N], ft[N];
         unpack16<T>(rl, fl);
         unpack16<T>(rr, fr);
@@ -135,6 +155,35 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
         nt_store16(pack16<T>(fr), reinterpret_cast<uint4*>(r) + v);
         nt_store16(ot, reinterpret_cast<uint4*>(t) + v);
         nt_store16(ot, reinterpret_cast<uint4*>(w) + v);         // W = t (clone)
+    };
+    auto one = [&](int64_t v) {
+        uint32_t bm[N], bl[N], br[N];
+        load_bytes<T>(pm + v * N, bm);
+        load_bytes<T>(pl + v * N, bl);
+        load_bytes<T>(pr + v * N, br);
+        body(v, bm, bl, br, reinterpret_cast<const uint4*>(l)[v], reinterpret_cast<const uint4*>(r)[v],
+             reinterpret_cast<const uint4*>(w)[v]);
+    };
+    // U vectors per tensor per iteration, all loads issued before any is consumed
+    for (int64_t v = e0 / N + (int64_t)blockIdx.x * kBlock + threadIdx.x; v < v1; v += stride * U) {
+        if (v + (U - 1) * stride < v1) {
+            uint32_t bm[U][N], bl[U][N], br[U][N];
+            uint4 rl[U], rr[U], rw[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int64_t u = v + k * stride;
+                load_bytes<T>(pm + u * N, bm[k]);
+                load_bytes<T>(pl + u * N, bl[k]);
+                load_bytes<T>(pr + u * N, br[k]);
+                rl[k] = reinterpret_cast<const uint4*>(l)[u];
+                rr[k] = reinterpret_cast<const uint4*>(r)[u];
+                rw[k] = reinterpret_cast<const uint4*>(w)[u];
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) body(v + k * stride, bm[k], bl[k], br[k], rl[k], rr[k], rw[k]);
+        } else {
+            for (int64_t u = v; u < v1; u += stride) one(u);
+        }
     }
     if (e1 == n && blockIdx.x == 0 && threadIdx.x < n - nvec * N) {
         const int64_t j = nvec * N + threadIdx.x;
@@ -167,7 +216,7 @@ static int mix_impl(void* t, const void* l, const void* r, const void* w, int n,
     if (!aligned16(t) || !aligned16(l) || !aligned16(r) || !aligned16(w)) return BAGUA_ERR_UNSUPPORTED;
     const int nblk = ws ? minmax_partials_blocks(n, Vec<T>::N, 1, ws_bytes) : 0;
     if (nblk < 1) return BAGUA_ERR_WORKSPACE;
-    launch(ring_mix_kernel<T>, dim3(nblk), dim3(kBlock), 0, s, static_cast<S*>(t),
+    launch(ring_mix_kernel<T, kMixUnroll>, dim3(nblk), dim3(kBlock), 0, s, static_cast<S*>(t),
                        static_cast<const S*>(l), static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13,
                        f53, static_cast<uint2*>(ws));
     return check_launch();
@@ -189,7 +238,7 @@ static int apply_impl(const uint8_t* mine, const uint8_t* from_left, const uint8
     int64_t blocks = ((int64_t)(e1 - e0) / N + kBlock - 1) / kBlock;
     if (blocks > 2 * kTargetBlocks) blocks = 2 * kTargetBlocks;
     if (blocks < 1) blocks = 1;
-    launch(ring_apply_kernel<T>, dim3(blocks), dim3(kBlock), 0, s, mine, from_left, from_right,
+    launch(ring_apply_kernel<T, kApplyUnroll>, dim3(blocks), dim3(kBlock), 0, s, mine, from_left, from_right,
            static_cast<S*>(t), static_cast<S*>(w), static_cast<S*>(l), static_cast<S*>(r), (int64_t)n, (int64_t)e0,
            (int64_t)e1);
     return check_launch();
