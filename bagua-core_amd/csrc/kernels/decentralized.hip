@@ -76,21 +76,24 @@ __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* _
     const uint4* r4 = reinterpret_cast<const uint4*>(r);
     const uint4* w4 = reinterpret_cast<const uint4*>(w);
     // U vectors per tensor per iteration (4U x 16 B in flight per lane), all loads
-    // issued before any is consumed; the last partial iteration goes one by one
+    // issued before any is consumed; the last partial iteration goes one by one.
+    // All four streams load non-temporally: default-policy t/w loads (or l/r) were
+    // slower (profiles/r01_ring_mix_policy_ab.jsonl)
     for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nvec; v += stride * U) {
         if (v + (U - 1) * stride < nvec) {
             uint4 rt[U], rl[U], rr[U], rw[U];
 #pragma unroll
             for (int k = 0; k < U; ++k) {
-                rt[k] = t4[v + k * stride];
+                rt[k] = nt_load16(t4 + v + k * stride);
                 rl[k] = nt_load16(l4 + v + k * stride);
                 rr[k] = nt_load16(r4 + v + k * stride);
-                rw[k] = w4[v + k * stride];
+                rw[k] = nt_load16(w4 + v + k * stride);
             }
 #pragma unroll
             for (int k = 0; k < U; ++k) body(v + k * stride, rt[k], rl[k], rr[k], rw[k]);
         } else {
-            for (int64_t u = v; u < nvec; u += stride) body(u, t4[u], nt_load16(l4 + u), nt_load16(r4 + u), w4[u]);
+            for (int64_t u = v; u < nvec; u += stride)
+                body(u, nt_load16(t4 + u), nt_load16(l4 + u), nt_load16(r4 + u), nt_load16(w4 + u));
         }
     }
     if (blockIdx.x == 0 && threadIdx.x < n - nvec * N) {  // ragged tail
