@@ -41,6 +41,7 @@ METRIC = ("GiB/s fp32 gradient encode+decode (device-resident); "
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GiB = float(1 << 30)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+PMC_SUMMARY_ONEBIT = os.path.join(ROOT, "profiles", "r01_pmc_traffic_onebit.json")
 
 
 def parse():
@@ -62,13 +63,13 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(kernel: str, summary: str = PMC_SUMMARY):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
     summary (profiles/r01_pmc_traffic.json, produced by
     profiles/collect_pmc.py following MI355X_MICROARCH.md §HBM: FETCH_SIZE
     doubled for 16-B streaming reads, WRITE_SIZE as is), or None."""
     try:
-        with open(PMC_SUMMARY) as f:
+        with open(summary) as f:
             d = json.load(f)
         return d.get("per_launch_hbm_bytes", {}).get(kernel)
     except (OSError, ValueError):
@@ -185,7 +186,9 @@ def bench_codec(args, onebit: bool = False):
     per[dom] = dom_ms
     achieved = alg[dom] / (per[dom] * 1e-3) / 1e9
     step_alg = sum(alg)
-    traffic = pmc_traffic(names[dom]) if (args.dtype == "f32" and n == (1 << 26) and not onebit) else None
+    # the committed PMC passes are of the default 256 MiB f32 bench (MinMax and 1-bit)
+    traffic = (pmc_traffic(names[dom], PMC_SUMMARY_ONEBIT if onebit else PMC_SUMMARY)
+               if (args.dtype == "f32" and n == (1 << 26)) else None)
     roof = {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "alg_bytes_per_launch": alg[dom], "avg_launch_us": round(per[dom] * 1e3, 2),

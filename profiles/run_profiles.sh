@@ -20,6 +20,11 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch"
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > /dev/null
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > /dev/null
+# the same two counter passes of the 1-bit bench (config 3)
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_ob" -o run -- \
+    python3 bench.py --workload onebit --steps 5 --warmup 1 --no-cpu-baseline > /dev/null
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_ob" -o run -- \
+    python3 bench.py --workload onebit --steps 5 --warmup 1 --no-cpu-baseline > /dev/null
 # the two-pass encode (BAGUA_RESIDENT=0) for comparison
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_2p" -o twopass -- \
     python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --two-pass > "$OUT/twopass_under_rocprof.json"
@@ -34,6 +39,7 @@ timeout -k 10 120 python3 bench.py --dtype bf16 --no-cpu-baseline > "$OUT/b_code
 timeout -k 10 120 python3 bench.py --workload allreduce > "$OUT/b_ar1.json"
 timeout -k 10 200 python3 bench.py --workload host --steps 10 > "$OUT/b_host.json"
 # python3 profiles/collect_pmc.py "$OUT/fetch" "$OUT/write" "profiles/${R}_pmc_traffic.json"
+# python3 profiles/collect_pmc.py "$OUT/fetch_ob" "$OUT/write_ob" "profiles/${R}_pmc_traffic_onebit.json"
 # (run locally on the merged gpurun_out/: only gpurun_out/ returns from the box)
 # cp "$(find "$OUT/trace" -name '*kernel_stats.csv' | head -1)" "profiles/${R}_bench_n1_kernel_stats.csv"
 # (run locally on the merged gpurun_out/: only gpurun_out/ returns from the box)
