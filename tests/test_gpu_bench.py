@@ -1,0 +1,67 @@
+"""The bench.py contract the driver reads: ONE strict-JSON line on stdout with
+the metric, the whole-job value, the roofline of the dominant kernel and the
+CPU baseline (N = 1), for the default run and the other workloads.  Short
+runs (a few steps) in a child process; the numbers themselves are not checked
+here, only that they are present, finite and consistent with each other."""
+import json
+import math
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+METRIC = "GiB/s fp32 gradient encode+decode (device-resident); 1/2/4/8-GPU compressed all-reduce GiB/s"
+
+
+def run_bench(*args, timeout=150):
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, capture_output=True,
+                         text=True, timeout=timeout)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, f"stdout must be one JSON line, got {len(lines)}: {out.stdout[:500]}"
+    return json.loads(lines[0])
+
+
+def check_common(d, steps, warmup):
+    assert d["metric"] == METRIC and d["unit"] == "GiB/s"
+    assert d["n_gpus"] == 1 and d["steps"] == steps and d["warmup"] == warmup
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["vs_baseline"] is None
+    assert math.isfinite(d["value"]) and d["value"] > 0 and d["ms_per_step"] > 0
+    assert "workload" in d["config"]
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    # achieved = algorithmic bytes per launch / the launch's measured duration
+    assert abs(r["achieved"] - r["alg_bytes_per_launch"] / (r["avg_launch_us"] * 1e-6) / 1e9) < 0.01 * r["achieved"]
+
+
+def test_default_run_is_config2_with_cpu_baseline():
+    d = run_bench("--steps", "5", "--warmup", "2", "--cpu-seconds", "0.5")
+    check_common(d, 5, 2)
+    assert d["config"]["config_index"] == 2 and d["config"]["bucket_elements"] == 1 << 26
+    # value = 256 MiB of fp32 gradient per step
+    assert abs(d["value"] - 256 / 1024 / (d["ms_per_step"] * 1e-3)) < 0.01 * d["value"]
+    assert d["roofline"]["kernel"] == "minmax_resident_encode_kernel"
+    assert d["roofline"]["traffic"] and d["roofline"]["traffic"] > 0  # committed PMC summary
+    c = d["cpu_baseline"]
+    assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+
+
+def test_onebit_run():
+    d = run_bench("--workload", "onebit", "--steps", "5", "--warmup", "2", "--no-cpu-baseline")
+    check_common(d, 5, 2)
+    assert d["config"]["config_index"] == 3
+    assert d["roofline"]["kernel"] == "onebit_encode_kernel"
+
+
+def test_allreduce_run_single_rank():
+    d = run_bench("--workload", "allreduce", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+                  "--no-decentralized", timeout=200)
+    check_common(d, 3, 1)
+    assert d["config"]["config_index"] == 4 and d["config"]["parallelism"] == "dp1"
+    assert d["fp32_allreduce_gib_s"] > 0 and d["onebit_allreduce"]["ms_per_step"] > 0
+    assert "side_errors" not in d
