@@ -670,6 +670,8 @@ int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, i
         BAGUA_RES_LAUNCH(10)
         BAGUA_RES_LAUNCH(11)
 #undef BAGUA_RES_LAUNCH
+        default:
+            return BAGUA_ERR_UNSUPPORTED;  // a configuration without a launch: never silently skip the encode
     }
     return check_launch();
 }
