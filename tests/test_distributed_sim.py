@@ -1,4 +1,4 @@
-"""CPU multi-process tests (gloo, world_size 2 and 4) of the compressed
+"""CPU multi-process tests (gloo, world_size 2, 3, 4 and 8) of the compressed
 all-reduce and the ring exchange: real collectives carry the compressed
 bytes between processes; the result must equal the single-process
 simulation of the reference op sequence bit-for-bit on every rank, and all
@@ -40,7 +40,8 @@ def test_centralized_gloo(tmp_path, world, dtype, cs):
         assert np.array_equal(outs[r], outs[0])
 
 
-@pytest.mark.parametrize("world,dtype,cs,pieces", [(2, 0, 5000, 3), (4, 0, 1031 * 8, 4), (2, 2, 1536, 4)])
+@pytest.mark.parametrize("world,dtype,cs,pieces", [(2, 0, 5000, 3), (4, 0, 1031 * 8, 4), (2, 2, 1536, 4),
+                                                   (8, 0, 1031 * 8, 4)])  # the driver's N = 8
 def test_centralized_pieced_gloo(tmp_path, world, dtype, cs, pieces):
     """The pipelined op's per-piece byte ranges (real bagua_minmax_u8_piece_range) moved
     between gloo processes reproduce the unpieced op bit-for-bit."""
@@ -58,7 +59,8 @@ def test_centralized_pieced_gloo(tmp_path, world, dtype, cs, pieces):
         assert np.array_equal(np.load(tmp_path / f"out{r}.npy"), want[r].view(np.uint8)), f"rank {r}"
 
 
-@pytest.mark.parametrize("world,dtype,cs,pieces", [(2, 0, 5000, 3), (4, 0, 1024 * 9 + 7, 4), (3, 2, 2048, 4)])
+@pytest.mark.parametrize("world,dtype,cs,pieces", [(2, 0, 5000, 3), (4, 0, 1024 * 9 + 7, 4), (3, 2, 2048, 4),
+                                                   (8, 0, 1024 * 5 + 3, 3)])
 def test_centralized_onebit_pieced_gloo(tmp_path, world, dtype, cs, pieces):
     """The pipelined 1-bit op's per-piece byte ranges (real bagua_onebit_piece_range; headers
     after the last alltoall piece, with the first allgather piece) moved between gloo
