@@ -37,11 +37,14 @@ __device__ __forceinline__ float addmul(float x, float y, float f) {
     else return as_stored<T>(x + as_stored<T>(y * f));
 }
 
+// addmul<T> already returns a value rounded to T (the 16-bit path ends in
+// as_stored; f32 is stored as computed), and rounding is idempotent, so no
+// further rounding is applied between the steps
 template <typename T>
 __device__ __forceinline__ float mix(float t, float l, float r, float w, float f13, float f53) {
-    t = as_stored<T>(addmul<T>(t, l, f13));
-    t = as_stored<T>(addmul<T>(t, r, f13));
-    return as_stored<T>(addmul<T>(t, w, f53));
+    t = addmul<T>(t, l, f13);
+    t = addmul<T>(t, r, f13);
+    return addmul<T>(t, w, f53);
 }
 
 template <typename T, int U>
