@@ -65,6 +65,8 @@ KERNEL_SIGNATURES = {
     "bagua_minmax_u8_compress_stage": (_i32, [_i32, _i32, _vp, _i32, _i32, _i32, _vp, _sz, _vp, _sz, _i32, _vp]),
     "bagua_minmax_u8_resident_path": (_i32, [_i32, _vp, _i32, _i32, _i32, _vp, _sz, _i32, _vp]),
     "bagua_minmax_u8_resident_trace": (_i32, [_vp]),
+    "bagua_minmax_u8_release_stream": (_i32, [_vp]),
+    "bagua_minmax_u8_resident_slots_in_use": (_i32, [_i32]),
     "bagua_minmax_u8_decompress_reduce": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _vp]),
     "bagua_minmax_u8_reduce_requantize": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _vp, _sz, _i32, _vp, _sz,
                                                  _vp]),
@@ -124,7 +126,11 @@ CORE_SIGNATURES = {
     "bagua_stream_wait_event": (_i32, [_u64, _u64]),
     "bagua_pool_alloc": (_i32, [_i32, _sz, ctypes.POINTER(ctypes.c_uint64)]),
     "bagua_pool_free": (_i32, [_u64]),
+    "bagua_pool_free_after": (_i32, [_u64, ctypes.POINTER(ctypes.c_uint64), _i32]),
     "bagua_pool_trim": (_i32, [_i32]),
+    "bagua_pool_bytes_pending": (_sz, [_i32]),
+    "bagua_release_stream_resources": (_i32, [_i32, _u64]),
+    "bagua_stream_workspace_count": (_sz, []),
     "bagua_pool_bytes_in_use": (_sz, [_i32]),
     "bagua_pool_bytes_cached": (_sz, [_i32]),
     "bagua_compressed_size": (_sz, [_i32, _i32, _sz, _sz]),

@@ -42,7 +42,7 @@ class BaguaCommBackendPy:
         self._pending: "queue.Queue[_Scheduled]" = queue.Queue()
         self._ordered: list[BaguaBucketPy] = []
         self._mapping: dict[str, BaguaBucketPy] = {}
-        self._events: dict[int, int] = {}
+        self._events: dict[str, int] = {}  # ready event per tensor name
         self._current: Optional[tuple[_Scheduled, float]] = None
         self._failures: list[str] = []
         self._worker = threading.Thread(target=self._work, name="bagua-comm-worker", daemon=True)
@@ -73,12 +73,12 @@ class BaguaCommBackendPy:
             raise RuntimeError(f"TensorError: tensor {tensor.name()} is not registered in any bucket")
         bucket.mark_tensor_ready(tensor)
         if ready_cuda_event_ptr:
-            self._events[id(tensor)] = int(ready_cuda_event_ptr)
+            self._events[tensor.name()] = int(ready_cuda_event_ptr)
         while self._ordered[0].ready_for_comm():
             b = self._ordered.pop(0)
             b.reset_comm_ready()
             self._ordered.append(b)
-            evs = [self._events.pop(id(t), 0) for t in b.tensors()]
+            evs = [self._events.pop(t.name(), 0) for t in b.tensors()]
             item = _Scheduled(b, [e for e in evs if e])
             self._channel.put(item)
             self._pending.put(item)

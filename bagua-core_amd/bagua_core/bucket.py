@@ -92,7 +92,7 @@ class BaguaBucketPy:
         self.name = name
         self._tensors = list(tensors)
         self._ops: list = []
-        self._ready: dict[int, bool] = {}
+        self._ready: dict[str, bool] = {}  # by tensor name (unique per register_ordered_buckets)
 
     # ---- bookkeeping (lib.rs:371-486) ------------------------------------------
     def tensors(self) -> list:
@@ -148,10 +148,12 @@ class BaguaBucketPy:
 
     # ---- readiness (datatypes/mod.rs:1256-1266, 793-813) -------------------------
     def mark_tensor_ready(self, tensor: BaguaTensorPy) -> None:
-        self._ready[id(tensor)] = True
+        # keyed by name, as the reference keeps readiness on the shared tensor
+        # (datatypes/mod.rs:793-813): any wrapper of a registered tensor counts
+        self._ready[tensor.name()] = True
 
     def ready_for_comm(self) -> bool:
-        return all(self._ready.get(id(t), False) or t.name().startswith("bagua_padding_tensor")
+        return all(self._ready.get(t.name(), False) or t.name().startswith("bagua_padding_tensor")
                    for t in self._tensors)
 
     def reset_comm_ready(self) -> None:

@@ -59,6 +59,7 @@ class BaguaTensorPy:
         self._name = name
         self._pool_ptr = 0
         self._raw = None
+        self._streams: set[int] = set()
 
     # ---- construction from a pool buffer (compress output) ------------------
     @classmethod
@@ -68,12 +69,22 @@ class BaguaTensorPy:
         obj._name = name
         obj._raw = raw
         obj._pool_ptr = raw.ptr if owned else 0
+        obj._streams = set()
         return obj
+
+    def _used_on(self, stream: int) -> None:
+        """Record a stream that queued work reading or writing this buffer."""
+        if self._pool_ptr:
+            self._streams.add(int(stream))
 
     def __del__(self):
         ptr = getattr(self, "_pool_ptr", 0)
         if ptr:
-            N.C.bagua_pool_free(ptr)
+            # stream-ordered release: the block is reused only after the work
+            # already queued on every stream that touched it has completed
+            streams = sorted(getattr(self, "_streams", ()))
+            arr = (ctypes.c_uint64 * max(1, len(streams)))(*streams)
+            N.C.bagua_pool_free_after(ptr, arr, len(streams))
             self._pool_ptr = 0
 
     def raw(self) -> N.bagua_tensor_t:
@@ -120,7 +131,9 @@ class BaguaTensorPy:
         rc = N.C.bagua_tensor_compress(ctypes.byref(src), code, n_chunks, current_stream_ptr(src.device_id),
                                        target_chunk, ctypes.byref(out))
         N.check(rc, f"compress({method}, n_chunks={n_chunks}, target_chunk={target_chunk})")
-        return BaguaTensorPy._from_raw(out, "compressed_tensor", owned=True)
+        res = BaguaTensorPy._from_raw(out, "compressed_tensor", owned=True)
+        res._used_on(current_stream_ptr(src.device_id))
+        return res
 
     def decompress_from(self, method: str, n_chunks: int, compressed_buffer: "BaguaTensorPy") -> None:
         code = compression_code(method)
@@ -128,9 +141,10 @@ class BaguaTensorPy:
         if n_chunks <= 0 or dst.num_elem_allocated % n_chunks != 0:
             raise RuntimeError("compression tensor size % n_chunks must be 0")
         comp = compressed_buffer.raw()
-        rc = N.C.bagua_tensor_decompress_from(ctypes.byref(dst), code, n_chunks, ctypes.byref(comp),
-                                              current_stream_ptr(dst.device_id))
+        stream = current_stream_ptr(dst.device_id)
+        rc = N.C.bagua_tensor_decompress_from(ctypes.byref(dst), code, n_chunks, ctypes.byref(comp), stream)
         N.check(rc, f"decompress_from({method}, n_chunks={n_chunks})")
+        compressed_buffer._used_on(stream)
 
     # helpers of RawBaguaTensor used by the comm ops (datatypes/mod.rs:203-522)
     def reduce_mean_inplace(self, n_chunks: int, target_chunk: int) -> None:

@@ -21,9 +21,12 @@
 //           read last are the ones the 256 MiB Infinity Cache still holds),
 //           then the LDS part, then the VGPR part, and write header / slack.
 //
-// Per-launch state lives in a library-owned slot (one per stream) that is
-// never reset: launch k on a slot draws tickets [kG, (k+1)G) from a monotonic
-// counter, so its tag is k+1 (no memset node, graph-replay safe).
+// Per-launch state lives in a library-owned slot (one per stream; the
+// hipStreamPerThread sentinel gets one per host thread) that is never reset:
+// launch k on a slot draws tickets [kG, (k+1)G) from a monotonic counter, so
+// its tag is k+1 (no memset node, graph-replay safe).  A slot changes owner
+// (release, or LRU reclaim when all 64 are taken) only after an event recorded
+// behind its last launch has completed.
 //
 // Residency: the exchange needs every workgroup of a chunk resident at once.
 // The grid equals the CU count and the kernel admits one workgroup per CU,
@@ -40,8 +43,11 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <stdio.h>
+
 #include <map>
 #include <mutex>
+#include <thread>
 #include <utility>
 
 #include "codec_common.hpp"
@@ -455,13 +461,40 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
 // ------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------
+// Slot keys.  hipStreamPerThread is a sentinel that names a DIFFERENT real
+// stream on every host thread, so two threads launching on it must not share a
+// slot (their tickets and granules would interleave): the sentinel is keyed
+// together with the calling thread.  Every other handle is one stream.
+struct StreamKey {
+    hipStream_t s = nullptr;
+    std::thread::id tid{};
+    bool operator<(const StreamKey& o) const { return s != o.s ? s < o.s : tid < o.tid; }
+    bool operator==(const StreamKey& o) const { return s == o.s && tid == o.tid; }
+};
+static StreamKey stream_key(hipStream_t s) {
+    StreamKey k;
+    k.s = s;
+    if (s == hipStreamPerThread) k.tid = std::this_thread::get_id();
+    return k;
+}
+
+struct SlotState {
+    bool used = false;
+    StreamKey owner;
+    uint64_t last_use = 0;      // LRU clock
+    hipEvent_t done = nullptr;  // recorded after the owner's latest launch on this slot
+    bool recorded = false;
+};
+
 struct ResidentDevice {
     bool init = false, ok = false;
     int grid = 0;
     int clock_khz = 0;
     ResidentSlot* slots = nullptr;
-    int next_slot = 0;
-    std::map<hipStream_t, int> stream_slot;
+    SlotState state[kResSlots];
+    std::map<StreamKey, int> stream_slot;
+    uint64_t clock = 0;
+    bool warned_full = false;
 };
 static std::mutex g_res_mu;
 static uint64_t* g_res_trace = nullptr;  // bagua_minmax_u8_resident_trace
@@ -523,42 +556,78 @@ static int env_int(const char* name, int dflt) {
     return (e && *e) ? atoi(e) : dflt;
 }
 
-// slot of (device, stream), or nullptr when the resident path is unavailable
-static ResidentSlot* acquire_slot(int dev, hipStream_t s, int* grid, int* clock_khz) {
-    if (dev < 0 || dev >= 64) return nullptr;
-    std::lock_guard<std::mutex> lk(g_res_mu);
+// Per-device state (slot array zeroed once); false when the resident path is
+// unavailable on `dev`.  Caller holds g_res_mu.
+static bool device_ready(int dev) {
+    if (dev < 0 || dev >= 64) return false;
     ResidentDevice& d = g_res_dev[dev];
     if (!d.init) {
         d.init = true;
         int cus = 0, khz = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return nullptr;
-        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return nullptr;
-        if (cus < 1 || cus > kResMaxGrid || khz < 1) return nullptr;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return false;
+        if (cus < 1 || cus > kResMaxGrid || khz < 1) return false;
         void* p = nullptr;
         const size_t bytes = sizeof(ResidentSlot) * kResSlots;
-        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) return false;
         if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
             (void)hipFree(p);
-            return nullptr;
+            return false;
         }
         d.slots = static_cast<ResidentSlot*>(p);
         d.grid = cus;
         d.clock_khz = khz;
         d.ok = true;
     }
-    if (!d.ok) return nullptr;
-    auto it = d.stream_slot.find(s);
-    int idx;
+    return d.ok;
+}
+
+// Slot of stream `s` on `dev` (caller holds g_res_mu; device_ready(dev) is
+// true), or -1.  A new stream takes a free slot; when all kResSlots are owned
+// the least recently used one is reclaimed after its owner's last launch on it
+// has completed (its `done` event), so no two launches ever run on one slot at
+// once.  The ticket counter stays monotonic across owners.
+static int acquire_slot_locked(int dev, hipStream_t s) {
+    ResidentDevice& d = g_res_dev[dev];
+    const StreamKey key = stream_key(s);
+    int idx = -1;
+    auto it = d.stream_slot.find(key);
     if (it != d.stream_slot.end()) {
         idx = it->second;
     } else {
-        if (d.next_slot >= kResSlots) return nullptr;
-        idx = d.next_slot++;
-        d.stream_slot.emplace(s, idx);
+        for (int i = 0; i < kResSlots && idx < 0; ++i)
+            if (!d.state[i].used) idx = i;
+        if (idx < 0) {
+            idx = 0;
+            for (int i = 1; i < kResSlots; ++i)
+                if (d.state[i].last_use < d.state[idx].last_use) idx = i;
+            SlotState& old = d.state[idx];
+            if (old.recorded && hipEventSynchronize(old.done) != hipSuccess) {
+                (void)hipGetLastError();
+                return -1;
+            }
+            d.stream_slot.erase(old.owner);
+            if (!d.warned_full) {
+                d.warned_full = true;
+                fprintf(stderr,
+                        "[bagua-core] one-launch encode: %d streams in use on device %d; reclaiming the least "
+                        "recently used slot (release streams with bagua_minmax_u8_release_stream)\n",
+                        kResSlots, dev);
+            }
+        }
+        SlotState& st = d.state[idx];
+        if (!st.done && hipEventCreateWithFlags(&st.done, hipEventDisableTiming) != hipSuccess) {
+            st.done = nullptr;
+            (void)hipGetLastError();
+            return -1;
+        }
+        st.used = true;
+        st.owner = key;
+        st.recorded = false;
+        d.stream_slot.emplace(key, idx);
     }
-    *grid = d.grid;
-    *clock_khz = d.clock_khz;
-    return d.slots + idx;
+    d.state[idx].last_use = ++d.clock;
+    return idx;
 }
 
 // Launch plan of the one-launch encode; ok == false: not eligible (the caller
@@ -566,6 +635,7 @@ static ResidentSlot* acquire_slot(int dev, hipStream_t s, int* grid, int* clock_
 struct ResidentPlan {
     bool ok = false;
     int cfg = 0;
+    int dev = 0;
     size_t lds = 0;
     ResidentArgs a{};
 };
@@ -594,8 +664,13 @@ static ResidentPlan resident_plan(const void* input, int64_t in_num_elem, int64_
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return pl;
     int grid = 0, khz = 0;
-    ResidentSlot* slot = acquire_slot(dev, s, &grid, &khz);
-    if (!slot || nact > grid) return pl;
+    {
+        std::lock_guard<std::mutex> lk(g_res_mu);
+        if (!device_ready(dev)) return pl;
+        grid = g_res_dev[dev].grid;
+        khz = g_res_dev[dev].clock_khz;
+    }
+    if (nact > grid) return pl;
     const ResidentCfg& c = kResCfg[cfg];
     void* kern = resident_kernel_for<T>(cfg);
     const size_t lds = resident_lds_bytes(c);
@@ -627,7 +702,7 @@ static ResidentPlan resident_plan(const void* input, int64_t in_num_elem, int64_
     a.chunk_offset = chunk_offset;
     a.out_bytes = out_bytes;
     a.num_chunks = p;
-    a.slot = slot;
+    a.slot = nullptr;  // taken at launch (resident_compress_impl)
     // bounded wait: the exchange normally completes a few us after the slowest
     // workgroup's pass 1, which reads the active chunks; allow that pass to run
     // at as little as 0.5 TB/s before giving up (then the waiting workgroups
@@ -638,6 +713,7 @@ static ResidentPlan resident_plan(const void* input, int64_t in_num_elem, int64_
     a.trace = g_res_trace;
     pl.cfg = cfg;
     pl.lds = lds;
+    pl.dev = dev;
     pl.ok = true;
     return pl;
 }
@@ -646,8 +722,15 @@ static ResidentPlan resident_plan(const void* input, int64_t in_num_elem, int64_
 template <typename T>
 int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, int p, uint8_t* out,
                            int64_t out_bytes, int target, hipStream_t s) {
-    const ResidentPlan pl = resident_plan<T>(input, in_num_elem, cs, p, out, out_bytes, target, s);
+    ResidentPlan pl = resident_plan<T>(input, in_num_elem, cs, p, out, out_bytes, target, s);
     if (!pl.ok) return BAGUA_ERR_UNSUPPORTED;
+    // slot choice, launch and the slot's `done` record happen under one lock, so a
+    // reclaim (acquire_slot_locked) always sees the slot's latest launch
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    ResidentDevice& d = g_res_dev[pl.dev];
+    const int idx = acquire_slot_locked(pl.dev, s);
+    if (idx < 0) return BAGUA_ERR_UNSUPPORTED;
+    pl.a.slot = d.slots + idx;
     const ResidentArgs& a = pl.a;
     switch (pl.cfg) {
 #define BAGUA_RES_LAUNCH(I)                                                                                 \
@@ -673,7 +756,48 @@ int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, i
         default:
             return BAGUA_ERR_UNSUPPORTED;  // a configuration without a launch: never silently skip the encode
     }
-    return check_launch();
+    const int rc = check_launch();
+    if (rc == BAGUA_OK) {
+        SlotState& st = d.state[idx];
+        if (hipEventRecord(st.done, s) != hipSuccess) {
+            g_last_hip_error = (int)hipGetLastError();
+            return BAGUA_ERR_HIP;
+        }
+        st.recorded = true;
+    }
+    return rc;
+}
+
+// Drops the slot of stream `s` on every device after the stream's last
+// one-launch encode has completed.  Safe to call for streams that never ran
+// one; the next launch on `s` takes a slot again.
+int release_stream_slot(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    const StreamKey key = stream_key(s);
+    int rc = BAGUA_OK;
+    for (int dev = 0; dev < 64; ++dev) {
+        ResidentDevice& d = g_res_dev[dev];
+        if (!d.ok) continue;
+        auto it = d.stream_slot.find(key);
+        if (it == d.stream_slot.end()) continue;
+        SlotState& st = d.state[it->second];
+        if (st.recorded && hipEventSynchronize(st.done) != hipSuccess) {
+            g_last_hip_error = (int)hipGetLastError();
+            rc = BAGUA_ERR_HIP;
+            continue;  // still in flight or faulted: keep the slot owned
+        }
+        st.used = false;
+        st.recorded = false;
+        st.last_use = 0;
+        d.stream_slot.erase(it);
+    }
+    return rc;
+}
+
+int resident_slots_in_use(int dev) {
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    if (dev < 0 || dev >= 64 || !g_res_dev[dev].ok) return 0;
+    return (int)g_res_dev[dev].stream_slot.size();
 }
 
 template <typename T>
@@ -687,6 +811,12 @@ template int resident_compress_impl<F16>(const void*, int64_t, int64_t, int, uin
 template int resident_compress_impl<BF16>(const void*, int64_t, int64_t, int, uint8_t*, int64_t, int, hipStream_t);
 
 }  // namespace bagua
+
+extern "C" int bagua_minmax_u8_release_stream(bagua_stream_t stream) {
+    return bagua::release_stream_slot(static_cast<hipStream_t>(stream));
+}
+
+extern "C" int bagua_minmax_u8_resident_slots_in_use(int device_id) { return bagua::resident_slots_in_use(device_id); }
 
 extern "C" int bagua_minmax_u8_resident_trace(void* device_buffer) {
     std::lock_guard<std::mutex> lk(bagua::g_res_mu);

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include "bagua_core.h"
+
 #include <atomic>
 #include <cstddef>
 #include <vector>
@@ -63,6 +65,14 @@ struct BaguaSingleCommunicatorC {
         return 0;
     }
     ~BaguaSingleCommunicatorC() {
+        // per-stream workspaces and one-launch encode slots of the streams this
+        // communicator ran ops on (the side stream is destroyed right after);
+        // release waits for the streams, so an aborted communicator, whose
+        // streams may hold collectives that never complete, keeps them
+        if (!aborted.load()) {
+            (void)bagua_release_stream_resources(device_id, (uint64_t)(uintptr_t)stream);
+            if (side) (void)bagua_release_stream_resources(device_id, (uint64_t)(uintptr_t)side);
+        }
         for (hipEvent_t e : events) (void)hipEventDestroy(e);
         if (side) (void)hipStreamDestroy(side);
     }

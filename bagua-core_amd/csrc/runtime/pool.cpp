@@ -5,7 +5,9 @@
 // Size classes are 4 per power of two (<= 25 % slack), so a 1 GiB gradient
 // bucket and its ~256 MiB compressed buffer do not double in size the way a
 // power-of-two pool would on a 288 GB HBM device.  Blocks are reused per
-// class; bagua_pool_trim() returns cached blocks to HIP.
+// class; bagua_pool_trim() returns cached blocks to HIP.  A block freed with
+// bagua_pool_free_after() waits in a pending list until events recorded on
+// the given streams have completed (the pool itself is not stream-ordered).
 #include <hip/hip_runtime.h>
 
 #include <map>
@@ -29,9 +31,18 @@ size_t size_class(size_t bytes) {
     return c;
 }
 
+// a block freed behind queued work: reusable once every event has completed
+struct PendingBlock {
+    uint64_t ptr;
+    size_t cls;
+    std::vector<hipEvent_t> events;
+};
+
 struct DevicePool {
     std::map<size_t, std::vector<uint64_t>> free_blocks;  // class -> blocks
-    size_t in_use = 0, cached = 0;
+    std::vector<PendingBlock> pending;
+    std::vector<hipEvent_t> spare_events;
+    size_t in_use = 0, cached = 0, pending_bytes = 0;
 };
 
 struct Pool {
@@ -45,6 +56,33 @@ Pool& pool() {
     return *p;
 }
 
+// Moves pending blocks whose streams have drained to the free lists (P.mu held).
+void reap_pending(DevicePool& d, bool wait) {
+    size_t keep = 0;
+    for (size_t i = 0; i < d.pending.size(); ++i) {
+        PendingBlock& b = d.pending[i];
+        bool done = true;
+        for (hipEvent_t e : b.events) {
+            const hipError_t q = wait ? hipEventSynchronize(e) : hipEventQuery(e);
+            if (q == hipErrorNotReady) {
+                done = false;
+                break;
+            }
+            if (q != hipSuccess) (void)hipGetLastError();  // a faulted stream: the block is not read any more
+        }
+        if (!done) {
+            if (keep != i) d.pending[keep] = std::move(b);
+            ++keep;
+            continue;
+        }
+        for (hipEvent_t e : b.events) d.spare_events.push_back(e);
+        d.pending_bytes -= b.cls;
+        d.cached += b.cls;
+        d.free_blocks[b.cls].push_back(b.ptr);
+    }
+    d.pending.resize(keep);
+}
+
 }  // namespace
 
 int pool_alloc(int device_id, size_t bytes, uint64_t* out) {
@@ -54,6 +92,7 @@ int pool_alloc(int device_id, size_t bytes, uint64_t* out) {
     {
         std::lock_guard<std::mutex> g(P.mu);
         DevicePool& d = P.dev[device_id];
+        if (!d.pending.empty()) reap_pending(d, false);
         auto it = d.free_blocks.find(cls);
         if (it != d.free_blocks.end() && !it->second.empty()) {
             *out = it->second.back();
@@ -100,12 +139,54 @@ int pool_free(uint64_t ptr) {
     return BAGUA_OK;
 }
 
+int pool_free_after(uint64_t ptr, const uint64_t* streams, int n) {
+    if (!ptr) return BAGUA_OK;
+    if (n <= 0) return pool_free(ptr);
+    if (!streams) return BAGUA_ERR_INVALID_ARG;
+    Pool& P = pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.live.find(ptr);
+    if (it == P.live.end()) return BAGUA_ERR_INVALID_ARG;
+    const int dev = it->second.first;
+    const size_t cls = it->second.second;
+    DevicePool& d = P.dev[dev];
+    DeviceGuard guard(dev);
+    PendingBlock b{ptr, cls, {}};
+    for (int i = 0; i < n; ++i) {
+        hipEvent_t e = nullptr;
+        if (!d.spare_events.empty()) {
+            e = d.spare_events.back();
+            d.spare_events.pop_back();
+        } else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            e = nullptr;
+        }
+        if (!e || hipEventRecord(e, (hipStream_t)(uintptr_t)streams[i]) != hipSuccess) {
+            (void)hipGetLastError();
+            // cannot order the reuse behind the stream: wait for it here instead
+            if (e) d.spare_events.push_back(e);
+            (void)hipStreamSynchronize((hipStream_t)(uintptr_t)streams[i]);
+            continue;
+        }
+        b.events.push_back(e);
+    }
+    P.live.erase(it);
+    d.in_use -= cls;
+    d.pending_bytes += cls;
+    d.pending.push_back(std::move(b));
+    return BAGUA_OK;
+}
+
 int pool_trim(int device_id) {
     Pool& P = pool();
     std::vector<uint64_t> release;
     {
         std::lock_guard<std::mutex> g(P.mu);
         DevicePool& d = P.dev[device_id];
+        if (!d.pending.empty()) {
+            DeviceGuard guard(device_id);
+            reap_pending(d, true);
+        }
         for (auto& kv : d.free_blocks) {
             for (uint64_t p : kv.second) release.push_back(p);
             kv.second.clear();
@@ -117,6 +198,13 @@ int pool_trim(int device_id) {
     (void)hipDeviceSynchronize();  // a cached block may still be read by queued work
     for (uint64_t p : release) (void)hipFree((void*)(uintptr_t)p);
     return BAGUA_OK;
+}
+
+size_t pool_bytes_pending(int device_id) {
+    Pool& P = pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.dev.find(device_id);
+    return it == P.dev.end() ? 0 : it->second.pending_bytes;
 }
 
 size_t pool_bytes(int device_id, bool cached) {
@@ -132,7 +220,11 @@ size_t pool_bytes(int device_id, bool cached) {
 extern "C" {
 int bagua_pool_alloc(int device_id, size_t bytes, uint64_t* ptr) { return bagua::pool_alloc(device_id, bytes, ptr); }
 int bagua_pool_free(uint64_t ptr) { return bagua::pool_free(ptr); }
+int bagua_pool_free_after(uint64_t ptr, const uint64_t* streams, int n) {
+    return bagua::pool_free_after(ptr, streams, n);
+}
 int bagua_pool_trim(int device_id) { return bagua::pool_trim(device_id); }
+size_t bagua_pool_bytes_pending(int device_id) { return bagua::pool_bytes_pending(device_id); }
 size_t bagua_pool_bytes_in_use(int device_id) { return bagua::pool_bytes(device_id, false); }
 size_t bagua_pool_bytes_cached(int device_id) { return bagua::pool_bytes(device_id, true); }
 }

@@ -13,12 +13,17 @@ namespace bagua {
 
 int pool_alloc(int device_id, size_t bytes, uint64_t* out);
 int pool_free(uint64_t ptr);
+int pool_free_after(uint64_t ptr, const uint64_t* streams, int n);
 int pool_trim(int device_id);
 size_t pool_bytes(int device_id, bool cached);
+size_t pool_bytes_pending(int device_id);
 
 // Per-(device, stream) scratch reused by every launch on that stream; stream
 // order makes reuse safe without host synchronisation.
 uint64_t stream_workspace(int device_id, uint64_t stream, size_t bytes);
+// Frees the stream's workspace after the stream has drained (communicator teardown).
+int release_stream_workspace(int device_id, uint64_t stream);
+size_t stream_workspace_count();
 
 // RAII current-device switch (communicators/mod.rs:32-35 does cudaSetDevice)
 class DeviceGuard {

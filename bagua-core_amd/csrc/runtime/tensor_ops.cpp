@@ -12,6 +12,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 
 #include "bagua_core.h"
 #include "runtime_util.hpp"
@@ -30,12 +31,35 @@ int log_level() {
     return lvl;
 }
 
+// Workspace key: (device, stream handle, host thread when the handle is the
+// hipStreamPerThread sentinel, which names a different stream on every thread
+// and must not share one workspace between them).
+struct WorkspaceKey {
+    int device;
+    uint64_t stream;
+    std::thread::id tid;
+    bool operator<(const WorkspaceKey& o) const {
+        if (device != o.device) return device < o.device;
+        if (stream != o.stream) return stream < o.stream;
+        return tid < o.tid;
+    }
+};
+
+static WorkspaceKey workspace_key(int device_id, uint64_t stream) {
+    WorkspaceKey k{device_id, stream, std::thread::id()};
+    if ((hipStream_t)(uintptr_t)stream == hipStreamPerThread) k.tid = std::this_thread::get_id();
+    return k;
+}
+
+static std::mutex g_ws_mu;
+static std::map<WorkspaceKey, std::pair<uint64_t, size_t>>& workspaces() {
+    static auto* cache = new std::map<WorkspaceKey, std::pair<uint64_t, size_t>>();  // outlives static teardown
+    return *cache;
+}
+
 uint64_t stream_workspace(int device_id, uint64_t stream, size_t bytes) {
-    static std::mutex mu;
-    static std::map<std::pair<int, uint64_t>, std::pair<uint64_t, size_t>>* cache =
-        new std::map<std::pair<int, uint64_t>, std::pair<uint64_t, size_t>>();
-    std::lock_guard<std::mutex> g(mu);
-    auto& slot = (*cache)[{device_id, stream}];
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    auto& slot = workspaces()[workspace_key(device_id, stream)];
     if (slot.second >= bytes && slot.first) return slot.first;
     if (slot.first) {
         // growing: queued work on this stream may still read the old block
@@ -48,6 +72,22 @@ uint64_t stream_workspace(int device_id, uint64_t stream, size_t bytes) {
     if (pool_alloc(device_id, want, &p) != BAGUA_OK) return 0;
     slot = {p, want};
     return p;
+}
+
+int release_stream_workspace(int device_id, uint64_t stream) {
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    auto it = workspaces().find(workspace_key(device_id, stream));
+    if (it == workspaces().end()) return BAGUA_OK;
+    // queued work on the stream may still read the block
+    if (hipStreamSynchronize((hipStream_t)(uintptr_t)stream) != hipSuccess) return BAGUA_ERR_HIP;
+    if (it->second.first) pool_free(it->second.first);
+    workspaces().erase(it);
+    return BAGUA_OK;
+}
+
+size_t stream_workspace_count() {
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    return workspaces().size();
 }
 
 static bool codec_dtype(int d) { return is_float_dtype(d); }
@@ -200,6 +240,15 @@ int bagua_tensor_clone_from(const bagua_tensor_t* t, const bagua_tensor_t* o, ui
 }  // extern "C"
 
 extern "C" {
+int bagua_release_stream_resources(int device_id, uint64_t stream) {
+    DeviceGuard guard(device_id);
+    const int rc = release_stream_workspace(device_id, stream);
+    const int rk = bagua_minmax_u8_release_stream((void*)(uintptr_t)stream);
+    return rc != BAGUA_OK ? rc : rk;
+}
+
+size_t bagua_stream_workspace_count(void) { return stream_workspace_count(); }
+
 // datatypes/mod.rs:969-980: the comm stream waits for a tensor's ready event
 int bagua_stream_wait_event(uint64_t stream, uint64_t event) {
     if (!event) return BAGUA_OK;

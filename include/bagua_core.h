@@ -56,7 +56,20 @@ int bagua_stream_wait_event(uint64_t stream, uint64_t event);
 /* CUDA_DEVICE_MEMORY_POOL (resource_pool/mod.rs:53-60): size-classed reuse of hipMalloc'd blocks */
 int bagua_pool_alloc(int device_id, size_t bytes, uint64_t* ptr);
 int bagua_pool_free(uint64_t ptr);
+/* Stream-ordered free: the block is reused only after everything queued so far on
+ * each of `streams` (n of them; 0 = the null stream) has completed (an event per
+ * stream, queried at the next allocation).  For buffers that queued work may still
+ * read, e.g. a compressed tensor dropped right after a decompress_from. */
+int bagua_pool_free_after(uint64_t ptr, const uint64_t* streams, int n);
 int bagua_pool_trim(int device_id);
+/* Blocks freed with bagua_pool_free_after whose streams have not drained yet. */
+size_t bagua_pool_bytes_pending(int device_id);
+/* Drops `stream`'s per-stream workspace and its one-launch encode slot after the
+ * stream has drained.  Communicator teardown calls it for its streams; call it
+ * before destroying any other stream that ran codec calls. */
+int bagua_release_stream_resources(int device_id, uint64_t stream);
+/* Number of live per-stream workspaces (diagnostics). */
+size_t bagua_stream_workspace_count(void);
 size_t bagua_pool_bytes_in_use(int device_id);
 size_t bagua_pool_bytes_cached(int device_id);
 

@@ -85,6 +85,15 @@ int bagua_minmax_u8_resident_path(int dtype, const void* input, int input_num_el
  * start, end of pass 1, exchange done, end of pass 2, end of the streamed
  * part of pass 2, end of its LDS part.  NULL disarms. */
 int bagua_minmax_u8_resident_trace(void* device_buffer);
+/* The one-launch encode keeps a small device slot per stream (its ticket
+ * counter and min/max exchange granules; 64 per device).  hipStreamPerThread
+ * gets one slot per calling host thread.  Release drops the stream's slot once
+ * its last one-launch encode has completed (host wait on that launch only);
+ * when all slots are owned, the least recently used one is reclaimed the same
+ * way.  Call it before destroying a stream that ran encodes. */
+int bagua_minmax_u8_release_stream(bagua_stream_t stream);
+/* Streams currently holding a slot on `device_id` (tests and diagnostics). */
+int bagua_minmax_u8_resident_slots_in_use(int device_id);
 /* decompress_uint8_to_{f32,f16}_host (K:667-681) */
 int bagua_minmax_u8_decompress(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
                                int num_chunks, void* output, bagua_stream_t stream);
