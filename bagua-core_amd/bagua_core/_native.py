@@ -172,6 +172,8 @@ CORE_SIGNATURES = {
     "bagua_decentralized_low_precision_synchronous": (_i32, [_C, _T, _T, _T, _T, _i32]),
     "bagua_decentralized_low_precision_synchronous_unfused": (_i32, [_C, _T, _T, _T, _T, _i32]),
     "bagua_decentralized_low_precision_pipelined": (_i32, [_C, _T, _T, _T, _T, _i32, _i32]),
+    "bagua_ring_exchange_plan": (_i32, [_i32, _i32, _i32, _i32, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_sz)]),
+    "bagua_ring_exchange_ops": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),
 }
 
 K = type("K", (), {})()

@@ -25,7 +25,9 @@
 #include "comm_internal.hpp"
 #include "runtime_util.hpp"
 
+#include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 using namespace bagua;
 
@@ -363,6 +365,148 @@ int centralized_pipelined_onebit(BaguaSingleCommunicatorC* c, const bagua_tensor
     return finish_both(c, BAGUA_OK);
 }
 
+// ---- ring exchange schedule ------------------------------------------------
+// The reference sends the whole compressed bucket straight to both ring peers
+// (decentralized_low_precision_synchronous.rs:98-115).  On a fully connected
+// xGMI node that loads 2 of each GPU's 7 links and leaves 5 idle.  From 6
+// ranks on, each piece's bytes are cut into p slices: slices 0..2 go straight
+// to the peer, slice k >= 3 is sent to relay rank r + (k-1) (for the right
+// peer; r - (k-1) for the left one), which forwards it in the next group.
+// Per directed link offset o the load is then (a = 3/p direct, b = 1/p per
+// relay): o = +-1: a + b; o = +-2: 3b; others 4b, i.e. at most 4/p of the
+// payload per link (8 ranks: 1/2) instead of all of it.  The schedule is
+// deterministic and symmetric, and every transfer carries a key (hop, flow,
+// slice) so that both ends post the transfers between two ranks in the same
+// order (NCCL matches grouped p2p in posting order per pair).
+constexpr int kRingMinMultipath = 6;
+
+struct RingPlan {
+    int p = 1, r = 0, pieces = 1, groups = 1;
+    bool mp = false;
+    Chunking k;
+    size_t slot = 0;  // relay scratch bytes per slice
+};
+
+enum { kBufMine = 0, kBufLeft = 1, kBufRight = 2, kBufRelay = 3 };
+
+// p + 1 slice boundaries of bytes [lo, hi), inner ones on 64-B lines
+void ring_slices(size_t lo, size_t hi, int p, size_t* b) {
+    const size_t len = hi - lo;
+    b[0] = lo;
+    b[p] = hi;
+    for (int i = 1; i < p; ++i) {
+        size_t x = (lo + len * (size_t)i / (size_t)p) & ~(size_t)63;
+        if (x < b[i - 1]) x = b[i - 1];
+        b[i] = x < hi ? x : hi;
+    }
+}
+
+int ring_plan(int nranks, int rank, int chunk_size, int pieces, bool multipath, RingPlan* P) {
+    if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks || chunk_size < 0 || pieces < 1) return BAGUA_ERR_INVALID_ARG;
+    P->p = nranks;
+    P->r = rank;
+    P->pieces = pieces;
+    P->mp = multipath && nranks >= kRingMinMultipath;
+    P->groups = pieces + (P->mp ? 1 : 0);
+    P->k.p = 1;
+    P->k.cs = (size_t)chunk_size;
+    P->k.S = bagua_minmax_u8_compressed_bytes(BAGUA_DTYPE_F32, chunk_size, 1);  // align32(n) + 32 for every dtype
+    P->slot = 0;
+    if (P->mp) {
+        size_t b[65];
+        for (int q = 0; q < pieces; ++q) {
+            size_t lo, hi;
+            piece_bytes(P->k, pieces, q, &lo, &hi);
+            if (hi <= lo) continue;
+            ring_slices(lo, hi, nranks, b);
+            for (int i = 3; i < nranks; ++i)
+                if (b[i + 1] - b[i] > P->slot) P->slot = b[i + 1] - b[i];
+        }
+        P->slot = (P->slot + 63) & ~(size_t)63;
+    }
+    return BAGUA_OK;
+}
+
+size_t ring_relay_bytes(const RingPlan& P) { return P.mp ? 4 * (size_t)(P.p - 3) * P.slot : 0; }
+
+// transfers of group g: the direct slices and first hops of piece g (g < pieces),
+// the relays' second hops of piece g - 1 (multipath, g > 0)
+std::vector<bagua_p2p_op_t> ring_ops(const RingPlan& P, int g) {
+    std::vector<bagua_p2p_op_t> v;
+    const int p = P.p, r = P.r;
+    auto rk = [&](int x) { return ((x % p) + p) % p; };
+    auto key = [](int hop, int flow, int slice) { return hop * 4096 + flow * 2048 + slice; };
+    auto add = [&](int peer, int send, int buf, int k, size_t off, size_t len) {
+        if (len) v.push_back(bagua_p2p_op_t{peer, send, buf, k, (uint64_t)off, (uint64_t)len});
+    };
+    auto relay_off = [&](int q, int flow, int slice) {
+        return ((size_t)((q & 1) * 2 + flow) * (size_t)(p - 3) + (size_t)(slice - 3)) * P.slot;
+    };
+    const int left = rk(r - 1), right = rk(r + 1);
+    size_t b[65];
+    if (g < P.pieces) {
+        size_t lo, hi;
+        piece_bytes(P.k, P.pieces, g, &lo, &hi);
+        if (hi > lo) {
+            const size_t dhi = P.mp ? (ring_slices(lo, hi, p, b), b[3]) : hi;
+            // flow 0: towards the right peer (lands in its left buffer); flow 1: towards the left peer
+            add(right, 1, kBufMine, key(0, 0, 0), lo, dhi - lo);
+            add(left, 1, kBufMine, key(0, 1, 0), lo, dhi - lo);
+            add(left, 0, kBufLeft, key(0, 0, 0), lo, dhi - lo);
+            add(right, 0, kBufRight, key(0, 1, 0), lo, dhi - lo);
+            if (P.mp)
+                for (int i = 3; i < p; ++i) {
+                    const int d = i - 1;
+                    const size_t len = b[i + 1] - b[i];
+                    add(rk(r + d), 1, kBufMine, key(1, 0, i), b[i], len);
+                    add(rk(r - d), 1, kBufMine, key(1, 1, i), b[i], len);
+                    add(rk(r - d), 0, kBufRelay, key(1, 0, i), relay_off(g, 0, i), len);  // source r-d's slice
+                    add(rk(r + d), 0, kBufRelay, key(1, 1, i), relay_off(g, 1, i), len);  // source r+d's slice
+                }
+        }
+    }
+    if (P.mp && g > 0) {
+        const int q = g - 1;
+        size_t lo, hi;
+        piece_bytes(P.k, P.pieces, q, &lo, &hi);
+        if (hi > lo) {
+            ring_slices(lo, hi, p, b);
+            for (int i = 3; i < p; ++i) {
+                const int d = i - 1;
+                const size_t len = b[i + 1] - b[i];
+                add(rk(r - d + 1), 1, kBufRelay, key(2, 0, i), relay_off(q, 0, i), len);  // source r-d -> its right
+                add(rk(r + d - 1), 1, kBufRelay, key(2, 1, i), relay_off(q, 1, i), len);  // source r+d -> its left
+                add(rk(r + d - 1), 0, kBufLeft, key(2, 0, i), b[i], len);    // left peer's slice via (r-1)+d
+                add(rk(r - d + 1), 0, kBufRight, key(2, 1, i), b[i], len);   // right peer's slice via (r+1)-d
+            }
+        }
+    }
+    std::stable_sort(v.begin(), v.end(), [](const bagua_p2p_op_t& a, const bagua_p2p_op_t& c) {
+        if (a.peer != c.peer) return a.peer < c.peer;
+        if (a.is_send != c.is_send) return a.is_send > c.is_send;
+        return a.key < c.key;
+    });
+    return v;
+}
+
+// one group of the ring exchange on the side stream
+int ring_exchange_group(BaguaSingleCommunicatorC* c, const RingPlan& P, int g, uint8_t* const bufs[4]) {
+    const std::vector<bagua_p2p_op_t> ops = ring_ops(P, g);
+    if (ops.empty()) return BAGUA_OK;
+    hipStream_t s1 = c->side;
+    int rc = c->t->group_start();
+    for (const bagua_p2p_op_t& o : ops) {
+        if (rc) break;
+        uint8_t* ptr = bufs[o.buffer] + o.offset;
+        rc = o.is_send ? c->t->send(ptr, o.bytes, BAGUA_DTYPE_U8, o.peer, s1)
+                       : c->t->recv(ptr, o.bytes, BAGUA_DTYPE_U8, o.peer, s1);
+    }
+    const int rc_end = c->t->group_end();
+    return rc ? rc : rc_end;
+}
+
+bool ring_multipath_enabled(int p) { return p >= kRingMinMultipath && env_int("BAGUA_RING_MULTIPATH", 1) != 0; }
+
 }  // namespace
 
 extern "C" {
@@ -391,23 +535,6 @@ int bagua_centralized_full_precision_synchronous(BaguaSingleCommunicatorC* c, co
     return finish(c, rc);
 }
 
-// piece q of the ring exchange: bytes [lo, hi) of the whole-bucket segment to and
-// from both ring peers, one group on the side stream
-static int ring_exchange_range(BaguaSingleCommunicatorC* c, uint8_t* mine, uint8_t* lbuf, uint8_t* rbuf, size_t lo,
-                               size_t hi) {
-    if (hi <= lo) return BAGUA_OK;
-    const int p = (int)c->nranks, r = (int)c->rank;
-    const int lpeer = (r + p - 1) % p, rpeer = (r + 1) % p;
-    const size_t len = hi - lo;
-    hipStream_t s1 = c->side;
-    int rc = c->t->group_start();
-    if (!rc) rc = c->t->send(mine + lo, len, BAGUA_DTYPE_U8, lpeer, s1);
-    if (!rc) rc = c->t->send(mine + lo, len, BAGUA_DTYPE_U8, rpeer, s1);
-    if (!rc) rc = c->t->recv(lbuf + lo, len, BAGUA_DTYPE_U8, lpeer, s1);
-    if (!rc) rc = c->t->recv(rbuf + lo, len, BAGUA_DTYPE_U8, rpeer, s1);
-    const int rc_end = c->t->group_end();
-    return rc ? rc : rc_end;
-}
 
 static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, const bagua_tensor_t* weight,
                          const bagua_tensor_t* left, const bagua_tensor_t* right, int method, bool allow_fused,
@@ -447,13 +574,16 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
         rc = bagua_ring_mix_minmax(t->dtype, tp, lp, rp, wp, n, ws, wsb, sp);
         if (rc == BAGUA_OK) {
             if (pieces < 1) pieces = c->nranks == 1 ? 1 : auto_pieces((size_t)n);
-            if (pieces > 1) {
+            const bool multipath = ring_multipath_enabled((int)c->nranks);
+            if (pieces > 1 || multipath) {
                 // pipelined: quantise piece q -> exchange piece q (side stream) -> apply piece q;
-                // one header for the whole bucket, travelling with piece 0
-                Chunking k;
-                k.p = 1;
-                k.cs = (size_t)n;
-                k.S = S;
+                // one header for the whole bucket, travelling with piece 0.  Multipath: the
+                // relayed slices of piece q arrive with group q + 1.
+                RingPlan plan;
+                TRY(ring_plan((int)c->nranks, (int)c->rank, n, pieces, multipath, &plan));
+                if (plan.k.S != S) return finish(c, BAGUA_ERR_INVALID_ARG);
+                PoolBuffer relay;
+                if (ring_relay_bytes(plan)) TRY(relay.allocate(c->device_id, ring_relay_bytes(plan)));
                 if (c->ensure_side(2 * (size_t)pieces + 1)) return finish(c, BAGUA_ERR_HIP);
                 hipStream_t s1 = c->side;
                 hipEvent_t* quantised = c->events.data();
@@ -462,6 +592,7 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
                 uint8_t* mb = mine.as<uint8_t>();
                 uint8_t* lb = lbuf.as<uint8_t>();
                 uint8_t* rb = rbuf.as<uint8_t>();
+                uint8_t* const bufs[4] = {mb, lb, rb, relay.as<uint8_t>()};
                 HIP2(hipEventRecord(start, c->stream));
                 HIP2(hipStreamWaitEvent(s1, start, 0));
                 for (int q = 0; q < pieces; ++q) {
@@ -471,12 +602,11 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
                         TRY2(bagua_minmax_u8_quantize_range(t->dtype, tp, n, n, 1, mb, S, ws, wsb, -1, b, e, sp));
                     HIP2(hipEventRecord(quantised[q], c->stream));
                 }
-                for (int q = 0; q < pieces; ++q) {
-                    size_t lo, hi;
-                    piece_bytes(k, pieces, q, &lo, &hi);
-                    HIP2(hipStreamWaitEvent(s1, quantised[q], 0));
-                    TRY2(ring_exchange_range(c, mb, lb, rb, lo, hi));
-                    HIP2(hipEventRecord(exchanged[q], s1));
+                for (int g = 0; g < plan.groups; ++g) {
+                    if (g < pieces) HIP2(hipStreamWaitEvent(s1, quantised[g], 0));
+                    TRY2(ring_exchange_group(c, plan, g, bufs));
+                    const int done = plan.mp ? g - 1 : g;  // the piece this group completes
+                    if (done >= 0) HIP2(hipEventRecord(exchanged[done], s1));
                 }
                 for (int q = 0; q < pieces; ++q) {
                     int b, e;
@@ -526,6 +656,28 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
     TRY(bagua_tensor_add_inplace(t, weight, s));
     TRY(bagua_tensor_clone_from(weight, t, s));
     return finish(c, BAGUA_OK);
+}
+
+int bagua_ring_exchange_plan(int nranks, int rank, int chunk_size, int pieces, int multipath, int* groups,
+                             size_t* relay_bytes) {
+    RingPlan P;
+    const int rc = ring_plan(nranks, rank, chunk_size, pieces, multipath != 0, &P);
+    if (rc) return rc;
+    if (groups) *groups = P.groups;
+    if (relay_bytes) *relay_bytes = ring_relay_bytes(P);
+    return BAGUA_OK;
+}
+
+int bagua_ring_exchange_ops(int nranks, int rank, int chunk_size, int pieces, int multipath, int group,
+                            bagua_p2p_op_t* ops, int max_ops) {
+    RingPlan P;
+    const int rc = ring_plan(nranks, rank, chunk_size, pieces, multipath != 0, &P);
+    if (rc) return -rc;
+    if (group < 0 || group >= P.groups) return -BAGUA_ERR_INVALID_ARG;
+    const std::vector<bagua_p2p_op_t> v = ring_ops(P, group);
+    if (!ops || (int)v.size() > max_ops) return -BAGUA_ERR_INVALID_ARG;
+    std::copy(v.begin(), v.end(), ops);
+    return (int)v.size();
 }
 
 int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t,

@@ -28,6 +28,7 @@ import json
 import math
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -40,6 +41,7 @@ METRIC = ("GiB/s fp32 gradient encode+decode (device-resident); "
           "1/2/4/8-GPU compressed all-reduce GiB/s")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GiB = float(1 << 30)
+SIDE_TIMEOUT_S = 120.0  # N > 1 side measurements: abort the communicator instead of hanging
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 PMC_SUMMARY_ONEBIT = os.path.join(ROOT, "profiles", "r01_pmc_traffic_onebit.json")
 
@@ -391,12 +393,23 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
 
     def side(name, fn):
         # side measurements must not cost the headline line: an error that every rank
-        # raises alike (argument checks, an unsupported shape) is recorded instead
+        # raises alike (argument checks, an unsupported shape) is recorded instead, and a
+        # measurement that has not finished after SIDE_TIMEOUT_S aborts the communicator
+        # (ncclCommAbort: pending collectives return) so the line is still printed
+        def expire():
+            side_errors[name] = f"timed out after {SIDE_TIMEOUT_S} s; communicator aborted"
+            comm.abort()
+
+        timer = threading.Timer(SIDE_TIMEOUT_S, expire)
+        timer.daemon = True
+        timer.start()
         try:
             return timed(fn, max(3, args.steps // 2), max(1, args.warmup // 2))
         except Exception as e:  # noqa: BLE001
-            side_errors[name] = str(e)[:200]
+            side_errors.setdefault(name, str(e)[:200])
             return float("nan")
+        finally:
+            timer.cancel()
 
     t_c = timed(compressed_step, args.steps, args.warmup)
     t_u = side("unpieced", lambda: compressed_step(1))
@@ -437,10 +450,22 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
                     comm.handle, *[ctypes.byref(r) for r in draws], N.COMPRESSION_MINMAX_UINT8, pieces),
                     "decentralized")
 
+            def direct(fn):
+                # the reference's exchange: the whole payload straight to both ring peers
+                os.environ["BAGUA_RING_MULTIPATH"] = "0"
+                try:
+                    fn()
+                finally:
+                    os.environ.pop("BAGUA_RING_MULTIPATH", None)
+
+            multipath = world >= 6  # comm_ops.cpp kRingMinMultipath
+            t_dd = side("decentralized_direct", lambda: direct(dec_step)) if multipath else float("nan")
             t_d = side("decentralized", dec_step)
             t_du = side("decentralized_unpieced", lambda: dec_step(1))
             decentralized = {"config_index": 5, "elements_per_rank": nb, "dtype": "bf16",
+                             "exchange": "multipath (3/p direct, the rest relayed)" if multipath else "direct",
                              "ms_per_step": round(t_d * 1e3, 3), "unpieced_ms_per_step": round(t_du * 1e3, 3),
+                             "direct_exchange_ms_per_step": round(t_dd * 1e3, 3) if multipath else None,
                              "gib_s_per_rank": round(2.0 * nb / t_d / GiB, 2),
                              "gib_s_total": round(world * 2.0 * nb / t_d / GiB, 2)}
             del bufs, draws

@@ -166,6 +166,32 @@ int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* comm
 int bagua_decentralized_low_precision_pipelined(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,
                                                 const bagua_tensor_t* weight, const bagua_tensor_t* left_peer_weight,
                                                 const bagua_tensor_t* right_peer_weight, int method, int pieces);
+/* Ring exchange schedule of the fused decentralized op (host-only, no device work).
+ * The reference sends the whole compressed bucket straight to both ring peers
+ * (decentralized_low_precision_synchronous.rs:98-115), which loads 2 of a
+ * GPU's 7 xGMI links.  From nranks >= 6 (BAGUA_RING_MULTIPATH=0 disables) each
+ * piece's bytes are cut into nranks slices: 3 go straight to the peer, slice k
+ * (3 <= k < nranks) is relayed through rank +-(k-1), so every link carries at
+ * most 4/nranks of the payload (8 ranks: half) instead of all of it; the relay
+ * forwards in the next group, so there are pieces + 1 groups.  Bytes arrive
+ * unchanged: the op stays bit-identical.
+ * Fills `ops` (capacity max_ops) with group `group`'s transfers for a bucket of
+ * `chunk_size` elements (n_chunks = 1 MinMax segments) cut into `pieces`, sorted
+ * so the k-th transfer between two ranks is the same message on both sides
+ * (NCCL's in-order p2p matching); returns the count (< 0: error).  *relay_bytes
+ * receives the relay scratch size (bytes). */
+typedef struct bagua_p2p_op {
+    int32_t peer;
+    int32_t is_send;
+    int32_t buffer; /* 0 own payload, 1 left peer's payload, 2 right peer's payload, 3 relay scratch */
+    int32_t key;    /* (hop, flow, slice) order key */
+    uint64_t offset;
+    uint64_t bytes;
+} bagua_p2p_op_t;
+int bagua_ring_exchange_plan(int nranks, int rank, int chunk_size, int pieces, int multipath, int* groups,
+                             size_t* relay_bytes);
+int bagua_ring_exchange_ops(int nranks, int rank, int chunk_size, int pieces, int multipath, int group,
+                            bagua_p2p_op_t* ops, int max_ops);
 /* the reference's unfused op sequence (3 addmul, compress, 3 x decompress + add, clone), for A/B */
 int bagua_decentralized_low_precision_synchronous_unfused(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,
                                                           const bagua_tensor_t* weight,

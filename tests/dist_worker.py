@@ -9,6 +9,7 @@ moving the real compressed bytes between processes.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import numpy as np
@@ -194,6 +195,80 @@ def decentralized_rank(rank: int, world: int, port: int, inputs_path: str, out_d
         C.decompress_minmax_u8(lbuf.numpy(), 1, t, dtype)
         C.add_inplace(l, t, dtype)
         C.decompress_minmax_u8(rbuf.numpy(), 1, t, dtype)
+        C.add_inplace(r, t, dtype)
+        C.decompress_minmax_u8(mine, 1, t, dtype)
+        C.add_inplace(t, w, dtype)
+        w[...] = t
+        np.savez(os.path.join(out_dir, f"dec{rank}.npz"), t=t.view(np.uint8), w=w.view(np.uint8),
+                 l=l.view(np.uint8), r=r.view(np.uint8))
+    finally:
+        dist.destroy_process_group()
+
+
+class P2POp(ctypes.Structure):
+    """bagua_p2p_op_t (include/bagua_core.h)"""
+    _fields_ = [("peer", ctypes.c_int32), ("is_send", ctypes.c_int32), ("buffer", ctypes.c_int32),
+                ("key", ctypes.c_int32), ("offset", ctypes.c_uint64), ("bytes", ctypes.c_uint64)]
+
+
+def _core_lib():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return ctypes.CDLL(os.path.join(root, "bagua-core_amd", "lib", "libbagua_core.so"))
+
+
+def ring_plan(p: int, rank: int, n: int, pieces: int, multipath: bool) -> tuple[int, int]:
+    """(groups, relay scratch bytes) of bagua_ring_exchange_plan (host-only)."""
+    lib = _core_lib()
+    g, rb = ctypes.c_int(), ctypes.c_size_t()
+    assert lib.bagua_ring_exchange_plan(p, rank, n, pieces, int(multipath), ctypes.byref(g), ctypes.byref(rb)) == 0
+    return g.value, rb.value
+
+
+def ring_ops(p: int, rank: int, n: int, pieces: int, multipath: bool, group: int) -> list:
+    """Group `group`'s transfers from bagua_ring_exchange_ops (host-only):
+    [(peer, is_send, buffer, key, offset, bytes)] in posting order."""
+    lib = _core_lib()
+    cap = 8 * p + 16
+    arr = (P2POp * cap)()
+    cnt = lib.bagua_ring_exchange_ops(p, rank, n, pieces, int(multipath), group, arr, cap)
+    assert cnt >= 0, cnt
+    return [(o.peer, o.is_send, o.buffer, o.key, o.offset, o.bytes) for o in arr[:cnt]]
+
+
+def decentralized_multipath_rank(rank: int, world: int, port: int, inputs_path: str, out_dir: str, dtype: int,
+                                 pieces: int) -> None:
+    """The fused ring op's exchange (comm_ops.cpp ring_ops: direct slices + relayed slices,
+    relays forward one group later) executed with gloo point-to-point transfers; a
+    transfer is matched by its (hop, flow, slice) key, so the test checks the routing
+    itself.  Receive buffers are poisoned: every byte must arrive."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        with np.load(inputs_path, allow_pickle=False) as z:
+            t, w, l, r = (z[f"{k}{rank}"].copy() for k in "twlr")
+        n = t.size
+        f13, f53 = float(np.float32(1.0 / 3.0)), float(np.float32(-5.0 / 3.0))
+        C.addmul_inplace(t, l, dtype, f13)
+        C.addmul_inplace(t, r, dtype, f13)
+        C.addmul_inplace(t, w, dtype, f53)
+        mine = C.compress_minmax_u8(t, dtype, 1, -1)
+        groups, relay_bytes = ring_plan(world, rank, n, pieces, True)
+        bufs = [torch.from_numpy(mine), torch.full((mine.size,), 0xAB, dtype=torch.uint8),
+                torch.full((mine.size,), 0xAB, dtype=torch.uint8), torch.zeros(max(1, relay_bytes), dtype=torch.uint8)]
+        for g in range(groups):
+            reqs = []
+            for peer, is_send, buf, key, off, nbytes in ring_ops(world, rank, n, pieces, True, g):
+                view = bufs[buf][off:off + nbytes]
+                tag = g * 65536 + key
+                reqs.append(dist.isend(view.clone(), peer, tag=tag) if is_send else (dist.irecv(view, peer, tag=tag)))
+            for q in reqs:
+                q.wait()
+            dist.barrier()  # the relay scratch of group g is read in group g + 1 only
+        lbuf, rbuf = bufs[1].numpy(), bufs[2].numpy()
+        C.decompress_minmax_u8(lbuf, 1, t, dtype)
+        C.add_inplace(l, t, dtype)
+        C.decompress_minmax_u8(rbuf, 1, t, dtype)
         C.add_inplace(r, t, dtype)
         C.decompress_minmax_u8(mine, 1, t, dtype)
         C.add_inplace(t, w, dtype)

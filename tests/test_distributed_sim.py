@@ -92,3 +92,78 @@ def test_decentralized_ring_gloo(tmp_path, world):
         with np.load(tmp_path / f"dec{r}.npz", allow_pickle=False) as z:
             for k, wk in zip("twlr", want):
                 assert np.array_equal(z[k], wk[r].view(np.uint8)), f"rank {r} {k}"
+
+
+def _simulate_ring_exchange(p: int, n: int, pieces: int, multipath: bool, rng) -> dict:
+    """Runs bagua_ring_exchange_ops' schedule for all p ranks on host byte arrays,
+    matching grouped transfers per (sender, receiver) pair in posting order as
+    NCCL does; returns per-rank buffers and per-link byte counts."""
+    groups, relay = dist_worker.ring_plan(p, 0, n, pieces, multipath)
+    S = ((n + 31) // 32) * 32 + 32
+    bufs = [[rng.integers(0, 256, S, dtype=np.uint8), np.full(S, 0xAB, np.uint8), np.full(S, 0xAB, np.uint8),
+             np.zeros(max(1, relay), np.uint8)] for _ in range(p)]
+    link = {}
+    for g in range(groups):
+        ops = [dist_worker.ring_ops(p, r, n, pieces, multipath, g) for r in range(p)]
+        sends, recvs = {}, {}
+        for r in range(p):
+            for peer, is_send, buf, key, off, nb in ops[r]:
+                (sends if is_send else recvs).setdefault((r, peer) if is_send else (peer, r), []).append(
+                    (buf, key, off, nb))
+        assert sends.keys() == recvs.keys()
+        moves = []
+        for (src, dst), ss in sends.items():
+            rr = recvs[(src, dst)]
+            assert len(ss) == len(rr)
+            for (sb, skey, soff, snb), (rb, rkey, roff, rnb) in zip(ss, rr):
+                assert skey == rkey and snb == rnb, (g, src, dst)
+                moves.append((dst, rb, roff, bufs[src][sb][soff:soff + snb].copy()))
+                if src != dst:
+                    link[(src, dst)] = link.get((src, dst), 0) + snb
+        for dst, rb, roff, data in moves:  # a group's sends read what was there before it
+            bufs[dst][rb][roff:roff + data.size] = data
+    return {"bufs": bufs, "link": link, "S": S, "groups": groups}
+
+
+@pytest.mark.parametrize("p", [1, 2, 3, 5, 6, 7, 8, 12, 16])
+@pytest.mark.parametrize("pieces", [1, 3, 4])
+@pytest.mark.parametrize("multipath", [False, True])
+def test_ring_exchange_schedule(p, pieces, multipath):
+    """Host-only check of the ring exchange schedule (comm_ops.cpp ring_ops): every rank
+    ends with its left and right peers' payload byte for byte, matched transfers agree
+    on key and size, and with multipath from 6 ranks on no link carries more than
+    4/p of a payload (8 ranks: half; direct: all of it) plus slice rounding."""
+    rng = np.random.default_rng(p * 100 + pieces)
+    n = 200_003
+    sim = _simulate_ring_exchange(p, n, pieces, multipath, rng)
+    bufs, S = sim["bufs"], sim["S"]
+    for r in range(p):
+        assert np.array_equal(bufs[r][1], bufs[(r - 1) % p][0]), f"rank {r} left"
+        assert np.array_equal(bufs[r][2], bufs[(r + 1) % p][0]), f"rank {r} right"
+    assert sim["groups"] == pieces + (1 if multipath and p >= 6 else 0)
+    if p >= 3:
+        worst = max(sim["link"].values())
+        if multipath and p >= 6:
+            assert worst <= 4 * S / p + 64 * pieces * 4, (worst, S)
+        else:
+            assert worst == S
+
+
+@pytest.mark.parametrize("world,pieces,dtype", [(6, 3, 0), (8, 4, 0), (8, 1, 2)])  # the driver's N = 8
+def test_decentralized_multipath_gloo(tmp_path, world, pieces, dtype):
+    """The multipath ring exchange (relayed slices) between gloo processes reproduces the
+    reference op sequence bit-for-bit on every rank and tensor."""
+    oracle_c.build()
+    n = 30_011
+    rng = np.random.default_rng(world * 17 + pieces)
+    arrs = {k: [NP.from_f32((rng.standard_normal(n) * 1e-3).astype(np.float32), dtype) for _ in range(world)]
+            for k in "twlr"}
+    inputs = tmp_path / "in.npz"
+    np.savez(inputs, **{f"{k}{r}": arrs[k][r] for k in "twlr" for r in range(world)})
+    mp.spawn(dist_worker.decentralized_multipath_rank, args=(world, _free_port(), str(inputs), str(tmp_path), dtype,
+                                                             pieces), nprocs=world, join=True)
+    want = simulate.decentralized_low_precision(oracle_c, arrs["t"], arrs["w"], arrs["l"], arrs["r"], dtype)
+    for r in range(world):
+        with np.load(tmp_path / f"dec{r}.npz", allow_pickle=False) as z:
+            for k, wk in zip("twlr", want):
+                assert np.array_equal(z[k], wk[r].view(np.uint8)), f"rank {r} {k}"
