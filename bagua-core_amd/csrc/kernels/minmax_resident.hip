@@ -24,9 +24,12 @@
 // Per-launch state lives in a library-owned slot (one per stream; the
 // hipStreamPerThread sentinel gets one per host thread) that is never reset:
 // launch k on a slot draws tickets [kG, (k+1)G) from a monotonic counter, so
-// its tag is k+1 (no memset node, graph-replay safe).  A slot changes owner
-// (release, or LRU reclaim when all 64 are taken) only after an event recorded
-// behind its last launch has completed.
+// its tag is k+1 (no memset node, graph-replay safe).  Every workgroup bumps a
+// second counter once it is done with the slot (after the exchange), so the
+// host can tell when every launch it issued on a slot has let go of it; a
+// slot changes owner (release, or LRU reclaim when all 64 are taken) only then.
+// (An event recorded behind every launch cost 3-5 us per step, even without a
+// system-scope fence: profiles/r02_slot_event_ab.jsonl.)
 //
 // Residency: the exchange needs every workgroup of a chunk resident at once.
 // The grid equals the CU count and the kernel admits one workgroup per CU,
@@ -41,10 +44,10 @@
 // Bit-identity: the same per-element expressions as minmax_quantize_kernel;
 // the min/max is order-free, so slicing cannot change it.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
 
-#include <stdio.h>
-
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -59,8 +62,10 @@ constexpr int kResMaxGrid = 1024;
 constexpr int kResSlots = 64;
 
 struct ResidentSlot {
-    uint64_t ticket;                 // monotonic ticket counter
+    uint64_t ticket;                 // monotonic ticket counter (one per workgroup at its start)
     uint64_t pad0[7];
+    uint64_t drained;                // workgroups done with the slot (one per workgroup after the exchange)
+    uint64_t pad1[7];
     uint64_t gran[2 * kResMaxGrid];  // {tag << 32 | min key}, {tag << 32 | max key} per workgroup
 };
 static_assert(sizeof(ResidentSlot) % 64 == 0, "slot alignment");
@@ -260,7 +265,10 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
     __syncthreads();
     const uint32_t tag = scratch[2 * W];
     trace_stamp(a, g, 0);
-    if (g >= a.nact * a.bpc) return;  // idle: the grid is the CU count on every launch of the slot
+    if (g >= a.nact * a.bpc) {  // idle: the grid is the CU count on every launch of the slot
+        if (t == 0) __hip_atomic_fetch_add(&a.slot->drained, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
 
     const SliceGeom<T, BLOCK> s(a, g);
     const uint4* __restrict__ v = reinterpret_cast<const uint4*>(s.src + s.j0);
@@ -385,6 +393,9 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
         }
         __syncthreads();
     }
+    // every thread's granule reads are done (the barriers above): this workgroup
+    // has let go of the slot
+    if (t == 0) __hip_atomic_fetch_add(&a.slot->drained, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const float mn = from_min_space(scratch[2 * W + 2]), mx = from_max_space(scratch[2 * W + 3]);
     const QParams q = make_qparams(mn, mx);
     trace_stamp(a, g, 2);
@@ -481,9 +492,8 @@ static StreamKey stream_key(hipStream_t s) {
 struct SlotState {
     bool used = false;
     StreamKey owner;
-    uint64_t last_use = 0;      // LRU clock
-    hipEvent_t done = nullptr;  // recorded after the owner's latest launch on this slot
-    bool recorded = false;
+    uint64_t last_use = 0;  // LRU clock
+    uint64_t launched = 0;  // workgroups launched on the slot since it was zeroed
 };
 
 struct ResidentDevice {
@@ -491,6 +501,8 @@ struct ResidentDevice {
     int grid = 0;
     int clock_khz = 0;
     ResidentSlot* slots = nullptr;
+    hipStream_t probe = nullptr;   // private non-blocking stream for reading `drained`
+    uint64_t* probe_host = nullptr;  // pinned landing word
     SlotState state[kResSlots];
     std::map<StreamKey, int> stream_slot;
     uint64_t clock = 0;
@@ -574,6 +586,17 @@ static bool device_ready(int dev) {
             (void)hipFree(p);
             return false;
         }
+        void* h = nullptr;
+        if (hipHostMalloc(&h, sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) {
+            (void)hipFree(p);
+            return false;
+        }
+        if (hipStreamCreateWithFlags(&d.probe, hipStreamNonBlocking) != hipSuccess) {
+            (void)hipHostFree(h);
+            (void)hipFree(p);
+            return false;
+        }
+        d.probe_host = static_cast<uint64_t*>(h);
         d.slots = static_cast<ResidentSlot*>(p);
         d.grid = cus;
         d.clock_khz = khz;
@@ -582,10 +605,29 @@ static bool device_ready(int dev) {
     return d.ok;
 }
 
+// Waits until every workgroup launched on slot `idx` has let go of it (its
+// `drained` count reaches the launched count), reading the counter on the
+// device's private stream, so no other stream is synchronised.  Caller holds
+// g_res_mu.
+static int wait_slot_drained(int dev, int idx) {
+    ResidentDevice& d = g_res_dev[dev];
+    const uint64_t want = d.state[idx].launched;
+    for (;;) {
+        if (hipMemcpyAsync(d.probe_host, &d.slots[idx].drained, sizeof(uint64_t), hipMemcpyDeviceToHost, d.probe) !=
+                hipSuccess ||
+            hipStreamSynchronize(d.probe) != hipSuccess) {
+            g_last_hip_error = (int)hipGetLastError();
+            return BAGUA_ERR_HIP;
+        }
+        if (*d.probe_host >= want) return BAGUA_OK;
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
 // Slot of stream `s` on `dev` (caller holds g_res_mu; device_ready(dev) is
 // true), or -1.  A new stream takes a free slot; when all kResSlots are owned
-// the least recently used one is reclaimed after its owner's last launch on it
-// has completed (its `done` event), so no two launches ever run on one slot at
+// the least recently used one is reclaimed once every launch issued on it has
+// let go of it (wait_slot_drained), so no two launches ever run on one slot at
 // once.  The ticket counter stays monotonic across owners.
 static int acquire_slot_locked(int dev, hipStream_t s) {
     ResidentDevice& d = g_res_dev[dev];
@@ -602,10 +644,7 @@ static int acquire_slot_locked(int dev, hipStream_t s) {
             for (int i = 1; i < kResSlots; ++i)
                 if (d.state[i].last_use < d.state[idx].last_use) idx = i;
             SlotState& old = d.state[idx];
-            if (old.recorded && hipEventSynchronize(old.done) != hipSuccess) {
-                (void)hipGetLastError();
-                return -1;
-            }
+            if (wait_slot_drained(dev, idx) != BAGUA_OK) return -1;
             d.stream_slot.erase(old.owner);
             if (!d.warned_full) {
                 d.warned_full = true;
@@ -616,14 +655,8 @@ static int acquire_slot_locked(int dev, hipStream_t s) {
             }
         }
         SlotState& st = d.state[idx];
-        if (!st.done && hipEventCreateWithFlags(&st.done, hipEventDisableTiming) != hipSuccess) {
-            st.done = nullptr;
-            (void)hipGetLastError();
-            return -1;
-        }
         st.used = true;
         st.owner = key;
-        st.recorded = false;
         d.stream_slot.emplace(key, idx);
     }
     d.state[idx].last_use = ++d.clock;
@@ -724,8 +757,8 @@ int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, i
                            int64_t out_bytes, int target, hipStream_t s) {
     ResidentPlan pl = resident_plan<T>(input, in_num_elem, cs, p, out, out_bytes, target, s);
     if (!pl.ok) return BAGUA_ERR_UNSUPPORTED;
-    // slot choice, launch and the slot's `done` record happen under one lock, so a
-    // reclaim (acquire_slot_locked) always sees the slot's latest launch
+    // slot choice, launch and the slot's launched count happen under one lock, so a
+    // reclaim (acquire_slot_locked) always waits for the slot's latest launch
     std::lock_guard<std::mutex> lk(g_res_mu);
     ResidentDevice& d = g_res_dev[pl.dev];
     const int idx = acquire_slot_locked(pl.dev, s);
@@ -757,19 +790,12 @@ int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, i
             return BAGUA_ERR_UNSUPPORTED;  // a configuration without a launch: never silently skip the encode
     }
     const int rc = check_launch();
-    if (rc == BAGUA_OK) {
-        SlotState& st = d.state[idx];
-        if (hipEventRecord(st.done, s) != hipSuccess) {
-            g_last_hip_error = (int)hipGetLastError();
-            return BAGUA_ERR_HIP;
-        }
-        st.recorded = true;
-    }
+    if (rc == BAGUA_OK) d.state[idx].launched += (uint64_t)a.grid;  // each workgroup drains once
     return rc;
 }
 
-// Drops the slot of stream `s` on every device after the stream's last
-// one-launch encode has completed.  Safe to call for streams that never ran
+// Drops the slot of stream `s` on every device once the stream's one-launch
+// encodes have let go of it (wait_slot_drained).  Safe to call for streams that never ran
 // one; the next launch on `s` takes a slot again.
 int release_stream_slot(hipStream_t s) {
     std::lock_guard<std::mutex> lk(g_res_mu);
@@ -781,13 +807,11 @@ int release_stream_slot(hipStream_t s) {
         auto it = d.stream_slot.find(key);
         if (it == d.stream_slot.end()) continue;
         SlotState& st = d.state[it->second];
-        if (st.recorded && hipEventSynchronize(st.done) != hipSuccess) {
-            g_last_hip_error = (int)hipGetLastError();
+        if (wait_slot_drained(dev, it->second) != BAGUA_OK) {
             rc = BAGUA_ERR_HIP;
-            continue;  // still in flight or faulted: keep the slot owned
+            continue;  // faulted: keep the slot owned
         }
         st.used = false;
-        st.recorded = false;
         st.last_use = 0;
         d.stream_slot.erase(it);
     }

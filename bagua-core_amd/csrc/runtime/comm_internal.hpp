@@ -14,6 +14,7 @@
 
 #include <atomic>
 #include <cstddef>
+#include <cstdlib>
 #include <vector>
 
 namespace bagua {
@@ -57,9 +58,17 @@ struct BaguaSingleCommunicatorC {
             side = nullptr;
             return -1;
         }
+        // cross-stream ordering on one device needs no system-scope fence (the
+        // producer kernel's own end-of-kernel release covers the device);
+        // BAGUA_EVENT_SYSTEM_FENCE=1 restores it (A/B)
+        static const unsigned flags = [] {
+            const char* v = std::getenv("BAGUA_EVENT_SYSTEM_FENCE");
+            return (v && *v && std::atoi(v) != 0) ? (unsigned)hipEventDisableTiming
+                                                   : (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence);
+        }();
         while (events.size() < n_events) {
             hipEvent_t e;
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -1;
+            if (hipEventCreateWithFlags(&e, flags) != hipSuccess) return -1;
             events.push_back(e);
         }
         return 0;

@@ -88,9 +88,9 @@ int bagua_minmax_u8_resident_trace(void* device_buffer);
 /* The one-launch encode keeps a small device slot per stream (its ticket
  * counter and min/max exchange granules; 64 per device).  hipStreamPerThread
  * gets one slot per calling host thread.  Release drops the stream's slot once
- * its last one-launch encode has completed (host wait on that launch only);
- * when all slots are owned, the least recently used one is reclaimed the same
- * way.  Call it before destroying a stream that ran encodes. */
+ * every workgroup launched on it has passed the min/max exchange (a device
+ * counter read on a private stream: no other stream is synchronised); when all
+ * slots are owned, the least recently used one is reclaimed the same way. */
 int bagua_minmax_u8_release_stream(bagua_stream_t stream);
 /* Streams currently holding a slot on `device_id` (tests and diagnostics). */
 int bagua_minmax_u8_resident_slots_in_use(int device_id);

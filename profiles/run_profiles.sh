@@ -7,7 +7,7 @@
 #    collect_pmc.py into <round>_pmc_traffic.json
 # Raw output stays under gpurun_out/prof; the summaries are copied to profiles/.
 set -euo pipefail
-R=${1:-r01}
+R=${1:-r02}
 OUT=gpurun_out/prof
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -46,3 +46,7 @@ timeout -k 10 200 python3 bench.py --workload host --steps 10 > "$OUT/b_host.jso
 # cp "$(find "$OUT/trace_ob" -name '*kernel_stats.csv' | head -1)" "profiles/${R}_onebit_kernel_stats.csv"
 # cp "$OUT/codec_under_rocprof.json" "profiles/${R}_bench_n1_under_rocprof.json"
 echo "profiles written for $R"
+# small buckets through the whole op at p = 1 (host/launch overhead per op)
+for e in 1048576 6553600 26214400; do
+  timeout -k 10 120 python3 bench.py --workload allreduce --elements $e --steps 50 --no-decentralized > "$OUT/b_ar1_small_$e.json"
+done
