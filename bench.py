@@ -42,6 +42,7 @@ METRIC = ("GiB/s fp32 gradient encode+decode (device-resident); "
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GiB = float(1 << 30)
 SIDE_TIMEOUT_S = 120.0  # N > 1 side measurements: abort the communicator instead of hanging
+HEADLINE_TIMEOUT_S = 300.0  # N > 1 headline (pipelined op): abort, then measure the unpieced op
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 PMC_SUMMARY_ONEBIT = os.path.join(ROOT, "profiles", "r01_pmc_traffic_onebit.json")
 
@@ -350,11 +351,16 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     torch.cuda.set_device(dev)
     if world > 1 and not dist.is_initialized():
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    uid = [BaguaSingleCommunicatorPy.generate_nccl_unique_id_str() if rank == 0 else None]
-    if world > 1:
-        dist.broadcast_object_list(uid, src=0)
     comm_stream = torch.cuda.Stream(device=dev)
-    comm = BaguaSingleCommunicatorPy(rank, world, local_rank, comm_stream.cuda_stream, uid[0])
+
+    def make_comm():
+        # communicators/mod.rs:25-60: rank 0's base64 ncclUniqueId, shared over gloo
+        uid = [BaguaSingleCommunicatorPy.generate_nccl_unique_id_str() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        return BaguaSingleCommunicatorPy(rank, world, local_rank, comm_stream.cuda_stream, uid[0])
+
+    comm = make_comm()
     n = args.elements or (1 << 28)
     n -= n % world
     g = torch.Generator(device=dev).manual_seed(0x5EED + rank)
@@ -411,7 +417,42 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         finally:
             timer.cancel()
 
-    t_c = timed(compressed_step, args.steps, args.warmup)
+    # The headline: the pipelined op.  Its multi-group RCCL schedule has run over the
+    # loopback transport, gloo and single-rank RCCL only; should it not
+    # finish on this node within HEADLINE_TIMEOUT_S, the communicator is aborted and
+    # the headline falls back to the unpieced op (the reference's one alltoall + one
+    # allgather) on a fresh communicator, recorded in headline_fallback.
+    headline_fallback = None
+    aborted = []
+
+    def expire_headline():
+        aborted.append(True)
+        comm.abort()
+
+    timer = threading.Timer(HEADLINE_TIMEOUT_S, expire_headline)
+    timer.daemon = True
+    timer.start()
+    try:
+        if os.environ.get("BAGUA_BENCH_FAIL_HEADLINE"):  # test hook: exercise the fallback below
+            comm.abort()
+        t_c = timed(compressed_step, args.steps, args.warmup)
+        err = "timed out; communicator aborted" if aborted else None
+    except Exception as e:  # noqa: BLE001 - an op error on every rank alike
+        err = str(e)[:200]
+    finally:
+        timer.cancel()
+    if world > 1:  # every rank takes the same branch (gloo all-reduce of the failure flag)
+        flag = torch.tensor([1.0 if err else 0.0])
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if flag.item() and not err:
+            err = "another rank failed"
+    if err:
+        if world == 1 and not os.environ.get("BAGUA_BENCH_FAIL_HEADLINE"):
+            raise RuntimeError(f"compressed all-reduce failed: {err}")
+        headline_fallback = {"pipelined_error": err, "headline": "unpieced op (pieces = 1)"}
+        comm = make_comm()
+        args.pieces = 1
+        t_c = timed(lambda: compressed_step(1), args.steps, args.warmup)
     t_u = side("unpieced", lambda: compressed_step(1))
     t_f = side("fp32_allreduce", fp32_step)
     # the same all-reduce with the 1-bit sign+scale codec (this repo's extension:
@@ -527,6 +568,8 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
              "per_kernel_us": {nm: round(t * 1e3, 2) for nm, t in zip(names, per)}}
     if side_errors:
         extra["side_errors"] = side_errors
+    if headline_fallback:
+        extra["headline_fallback"] = headline_fallback
     del comm
     return value, t_c * 1e3, roof, cfg, extra
 
