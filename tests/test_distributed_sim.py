@@ -128,20 +128,20 @@ def _simulate_ring_exchange(p: int, n: int, pieces: int, multipath: bool, rng) -
 @pytest.mark.parametrize("p", [1, 2, 3, 5, 6, 7, 8, 12, 16])
 @pytest.mark.parametrize("pieces", [1, 3, 4])
 @pytest.mark.parametrize("multipath", [False, True])
-def test_ring_exchange_schedule(p, pieces, multipath):
+@pytest.mark.parametrize("n", [200_003, 100])  # 100: slices of a few bytes, most of them empty
+def test_ring_exchange_schedule(p, pieces, multipath, n):
     """Host-only check of the ring exchange schedule (comm_ops.cpp ring_ops): every rank
     ends with its left and right peers' payload byte for byte, matched transfers agree
     on key and size, and with multipath from 6 ranks on no link carries more than
     4/p of a payload (8 ranks: half; direct: all of it) plus slice rounding."""
     rng = np.random.default_rng(p * 100 + pieces)
-    n = 200_003
     sim = _simulate_ring_exchange(p, n, pieces, multipath, rng)
     bufs, S = sim["bufs"], sim["S"]
     for r in range(p):
         assert np.array_equal(bufs[r][1], bufs[(r - 1) % p][0]), f"rank {r} left"
         assert np.array_equal(bufs[r][2], bufs[(r + 1) % p][0]), f"rank {r} right"
     assert sim["groups"] == pieces + (1 if multipath and p >= 6 else 0)
-    if p >= 3:
+    if p >= 3 and n > 100_000:
         worst = max(sim["link"].values())
         if multipath and p >= 6:
             assert worst <= 4 * S / p + 64 * pieces * 4, (worst, S)
