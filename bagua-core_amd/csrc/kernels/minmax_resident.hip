@@ -501,8 +501,7 @@ struct ResidentDevice {
     int grid = 0;
     int clock_khz = 0;
     ResidentSlot* slots = nullptr;
-    hipStream_t probe = nullptr;   // private non-blocking stream for reading `drained`
-    uint64_t* probe_host = nullptr;  // pinned landing word
+    uint64_t* probe_host = nullptr;  // pinned landing word for reading `drained`
     SlotState state[kResSlots];
     std::map<StreamKey, int> stream_slot;
     uint64_t clock = 0;
@@ -586,13 +585,11 @@ static bool device_ready(int dev) {
             (void)hipFree(p);
             return false;
         }
+        // no private stream: with GPU_MAX_HW_QUEUES = 4 one more stream shares a
+        // hardware queue with the caller's streams and serialised, e.g., the
+        // host-resident bench's H2D and D2H copies (43 -> 27 GiB/s)
         void* h = nullptr;
         if (hipHostMalloc(&h, sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) {
-            (void)hipFree(p);
-            return false;
-        }
-        if (hipStreamCreateWithFlags(&d.probe, hipStreamNonBlocking) != hipSuccess) {
-            (void)hipHostFree(h);
             (void)hipFree(p);
             return false;
         }
@@ -606,16 +603,18 @@ static bool device_ready(int dev) {
 }
 
 // Waits until every workgroup launched on slot `idx` has let go of it (its
-// `drained` count reaches the launched count), reading the counter on the
-// device's private stream, so no other stream is synchronised.  Caller holds
-// g_res_mu.
-static int wait_slot_drained(int dev, int idx) {
+// `drained` count reaches the launched count).  The counter is read with a copy
+// on `via` (a stream the caller knows to be alive: the stream being released,
+// or the stream about to take the slot over), which is drained first; the old
+// owner's launches may run on another stream, hence the loop.  Caller holds
+// g_res_mu.  Rare: release, or more than kResSlots streams.
+static int wait_slot_drained(int dev, int idx, hipStream_t via) {
     ResidentDevice& d = g_res_dev[dev];
     const uint64_t want = d.state[idx].launched;
     for (;;) {
-        if (hipMemcpyAsync(d.probe_host, &d.slots[idx].drained, sizeof(uint64_t), hipMemcpyDeviceToHost, d.probe) !=
+        if (hipMemcpyAsync(d.probe_host, &d.slots[idx].drained, sizeof(uint64_t), hipMemcpyDeviceToHost, via) !=
                 hipSuccess ||
-            hipStreamSynchronize(d.probe) != hipSuccess) {
+            hipStreamSynchronize(via) != hipSuccess) {
             g_last_hip_error = (int)hipGetLastError();
             return BAGUA_ERR_HIP;
         }
@@ -644,7 +643,7 @@ static int acquire_slot_locked(int dev, hipStream_t s) {
             for (int i = 1; i < kResSlots; ++i)
                 if (d.state[i].last_use < d.state[idx].last_use) idx = i;
             SlotState& old = d.state[idx];
-            if (wait_slot_drained(dev, idx) != BAGUA_OK) return -1;
+            if (wait_slot_drained(dev, idx, s) != BAGUA_OK) return -1;
             d.stream_slot.erase(old.owner);
             if (!d.warned_full) {
                 d.warned_full = true;
@@ -807,7 +806,7 @@ int release_stream_slot(hipStream_t s) {
         auto it = d.stream_slot.find(key);
         if (it == d.stream_slot.end()) continue;
         SlotState& st = d.state[it->second];
-        if (wait_slot_drained(dev, it->second) != BAGUA_OK) {
+        if (wait_slot_drained(dev, it->second, s) != BAGUA_OK) {
             rc = BAGUA_ERR_HIP;
             continue;  // faulted: keep the slot owned
         }

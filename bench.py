@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--two-pass", action="store_true",
                     help="codec workload: force the two-kernel MinMax encode (BAGUA_RESIDENT=0) for A/B")
     ap.add_argument("--no-decentralized", action="store_true", help="skip the config-5 side measurement (N > 1)")
+    ap.add_argument("--copy-chunks", type=int, default=2,
+                    help="host workload: pieces per H2D / D2H copy (1 = one copy each way per bucket)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the cpu_baseline leg")
     return ap.parse_args()
 
@@ -259,6 +261,22 @@ def bench_host(args):
     ev_cmp = [torch.cuda.Event() for _ in range(2)]
     ev_out = [torch.cuda.Event() for _ in range(2)]
 
+    chunks = max(1, args.copy_chunks)
+
+    def h2d(b):
+        # the copies go in `chunks` pieces: one 256 MiB H2D next to one D2H sometimes
+        # does not overlap at all (9.4 ms for the pair vs 4.7 ms each), two pieces per
+        # copy overlap every time (5.6 ms; bagua-core_amd/tools/pcie_probe.py,
+        # profiles/r02_host_copy_ab.jsonl)
+        step = (n + chunks - 1) // chunks
+        for lo in range(0, n, step):
+            x[b][lo:lo + step].copy_(src[lo:lo + step], non_blocking=True)
+
+    def d2h(b):
+        step = (n + chunks - 1) // chunks
+        for lo in range(0, n, step):
+            dst[b][lo:lo + step].copy_(y[b][lo:lo + step], non_blocking=True)
+
     def overlapped(steps):
         torch.cuda.synchronize()
         for b in range(2):  # start with every buffer free
@@ -269,7 +287,7 @@ def bench_host(args):
             b = i % 2
             s_in.wait_event(ev_cmp[b])       # x[b] consumed by the codec of bucket i-2
             with torch.cuda.stream(s_in):
-                x[b].copy_(src, non_blocking=True)
+                h2d(b)
             ev_in[b].record(s_in)
             s_cmp.wait_event(ev_in[b])
             s_cmp.wait_event(ev_out[b])      # y[b] drained by the D2H of bucket i-2
@@ -277,7 +295,7 @@ def bench_host(args):
             ev_cmp[b].record(s_cmp)
             s_out.wait_event(ev_cmp[b])
             with torch.cuda.stream(s_out):
-                dst[b].copy_(y[b], non_blocking=True)
+                d2h(b)
             ev_out[b].record(s_out)
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / steps
@@ -299,7 +317,7 @@ def bench_host(args):
     ok = torch.equal(dst[(args.steps - 1) % 2], y[(args.steps - 1) % 2].cpu())
     value = 4.0 * n / t_ovl / GiB
     cfg = {"workload": f"minmax_uint8_encode_decode_{4 * n >> 20}MiB_fp32_bucket_host_resident", "bucket_elements": n,
-           "n_chunks": 1, "config_index": 2, "buffers": "pinned host fp32 in/out"}
+           "n_chunks": 1, "config_index": 2, "buffers": "pinned host fp32 in/out", "copy_pieces": chunks}
     extra = {"serial_gib_s": round(4.0 * n / t_ser / GiB, 2), "serial_ms_per_bucket": round(t_ser * 1e3, 3),
              "overlapped_gib_s": round(value, 2), "h2d_gib_s": round(copy_rate(True, 5), 2),
              "d2h_gib_s": round(copy_rate(False, 5), 2), "result_copied_back_intact": bool(ok)}
