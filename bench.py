@@ -35,6 +35,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "bagua-core_amd"))
 sys.path.insert(0, ROOT)
 
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    # N > 1: the pipelined ops overlap a side stream (RCCL pieces) with the codec
+    # stream, and RCCL keeps internal streams of its own.  HIP maps streams onto
+    # GPU_MAX_HW_QUEUES hardware queues round-robin (4 by default); two streams on
+    # one queue serialise (profiles/r02_host_copy_ab.jsonl shows what that costs).
+    # 8 keeps the op's streams on queues of their own.  Set before HIP initialises.
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import torch  # noqa: E402
 
 METRIC = ("GiB/s fp32 gradient encode+decode (device-resident); "
