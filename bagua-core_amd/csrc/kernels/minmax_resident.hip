@@ -491,6 +491,7 @@ static StreamKey stream_key(hipStream_t s) {
 
 struct SlotState {
     bool used = false;
+    bool captured = false;  // a graph holds a launch on this slot: never reused (see below)
     StreamKey owner;
     uint64_t last_use = 0;  // LRU clock
     uint64_t launched = 0;  // workgroups launched on the slot since it was zeroed
@@ -637,11 +638,11 @@ static int acquire_slot_locked(int dev, hipStream_t s) {
         idx = it->second;
     } else {
         for (int i = 0; i < kResSlots && idx < 0; ++i)
-            if (!d.state[i].used) idx = i;
+            if (!d.state[i].used && !d.state[i].captured) idx = i;
         if (idx < 0) {
-            idx = 0;
-            for (int i = 1; i < kResSlots; ++i)
-                if (d.state[i].last_use < d.state[idx].last_use) idx = i;
+            for (int i = 0; i < kResSlots; ++i)
+                if (!d.state[i].captured && (idx < 0 || d.state[i].last_use < d.state[idx].last_use)) idx = i;
+            if (idx < 0) return -1;  // every slot is held by a captured graph
             SlotState& old = d.state[idx];
             if (wait_slot_drained(dev, idx, s) != BAGUA_OK) return -1;
             d.stream_slot.erase(old.owner);
@@ -762,6 +763,12 @@ int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, i
     ResidentDevice& d = g_res_dev[pl.dev];
     const int idx = acquire_slot_locked(pl.dev, s);
     if (idx < 0) return BAGUA_ERR_UNSUPPORTED;
+    // A launch captured into a graph keeps this slot's address: every replay draws
+    // tickets and bumps `drained` without the host knowing, so the slot can never
+    // be handed to another stream again (16 KiB stays with the graph).
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess) (void)hipGetLastError();
+    if (cap != hipStreamCaptureStatusNone) d.state[idx].captured = true;
     pl.a.slot = d.slots + idx;
     const ResidentArgs& a = pl.a;
     switch (pl.cfg) {
@@ -806,6 +813,10 @@ int release_stream_slot(hipStream_t s) {
         auto it = d.stream_slot.find(key);
         if (it == d.stream_slot.end()) continue;
         SlotState& st = d.state[it->second];
+        if (st.captured) {  // a graph still holds it: unmap the stream, never reuse the slot
+            d.stream_slot.erase(it);
+            continue;
+        }
         if (wait_slot_drained(dev, it->second, s) != BAGUA_OK) {
             rc = BAGUA_ERR_HIP;
             continue;  // faulted: keep the slot owned

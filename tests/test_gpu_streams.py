@@ -237,3 +237,39 @@ def test_backend_readiness_by_name(N):
     ev.record()
     backend.mark_communication_ready(other, ev.cuda_event)
     assert backend.wait_pending_comm_ops() == 1
+
+
+def test_resident_encode_replayed_from_a_graph(N, oracle_c):
+    """The one-launch encode captured into a HIP graph: every replay draws fresh
+    tickets (tags advance without the host) and stays bit-exact on new data; the
+    captured slot is never handed to another stream, even after a release."""
+    K = N.K
+    n, p = 1 << 22, 2
+    xs = [make_input(n, F32, seed=300 + i) for i in range(3)]
+    xt = to_dev(xs[0], F32)
+    out, ws, S, wsb = _buffers(K, n, p)
+    st = torch.cuda.Stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    assert K.bagua_minmax_u8_resident_path(F32, xt.data_ptr(), n, n // p, p, out.data_ptr(), S, -1, sp) == 1
+    # warm up outside capture (one-time attribute/occupancy setup)
+    assert K.bagua_minmax_u8_compress(F32, xt.data_ptr(), n, n // p, p, out.data_ptr(), S, ws.data_ptr(), wsb, -1,
+                                      sp) == 0
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        rc = K.bagua_minmax_u8_compress(F32, xt.data_ptr(), n, n // p, p, out.data_ptr(), S, ws.data_ptr(), wsb, -1,
+                                        sp)
+    assert rc == 0
+    for x in xs:
+        xt.copy_(torch.from_numpy(x).cuda())
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), oracle_c.compress_minmax_u8(x, F32, p))
+    used = K.bagua_minmax_u8_resident_slots_in_use(0)
+    assert K.bagua_minmax_u8_release_stream(sp) == 0
+    assert K.bagua_minmax_u8_resident_slots_in_use(0) == used - 1
+    # the graph still owns its slot: a replay after the release is still exact
+    xt.copy_(torch.from_numpy(xs[1]).cuda())
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), oracle_c.compress_minmax_u8(xs[1], F32, p))
