@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--two-pass", action="store_true",
                     help="codec workload: force the two-kernel MinMax encode (BAGUA_RESIDENT=0) for A/B")
     ap.add_argument("--no-decentralized", action="store_true", help="skip the config-5 side measurement (N > 1)")
+    ap.add_argument("--no-cold", action="store_true",
+                    help="codec workloads: skip the two-bucket alternating side line")
     ap.add_argument("--copy-chunks", type=int, default=2,
                     help="host workload: pieces per H2D / D2H copy (1 = one copy each way per bucket)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the cpu_baseline leg")
@@ -114,9 +116,14 @@ def bench_codec(args, onebit: bool = False):
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     xp, yp, cp, wp = x.data_ptr(), y.data_ptr(), comp.data_ptr(), ws.data_ptr()
 
+    launches_for = None
     if onebit:
         # the compress call launches encode then finalize; the timing hook times its first kernel
         names = ["onebit_encode_kernel", "onebit_decode_kernel"]
+
+        def launches_for(xq, yq, cq):
+            return [lambda: K.bagua_onebit_compress(dcode, xq, n, n, p, cq, S, wp, ws_bytes, -1, sp),
+                    lambda: K.bagua_onebit_decompress(dcode, cq, S, n, p, yq, sp)]
 
         def launches():
             return [lambda: K.bagua_onebit_compress(dcode, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
@@ -126,6 +133,10 @@ def bench_codec(args, onebit: bool = False):
         # one-launch encode (minmax_resident.hip): pass 1 keeps part of the bucket in
         # VGPRs/LDS across the min/max exchange (a single kernel per compress call)
         names = ["minmax_resident_encode_kernel", "minmax_dequantize_kernel"]
+
+        def launches_for(xq, yq, cq):
+            return [lambda: K.bagua_minmax_u8_compress(dcode, xq, n, n, p, cq, S, wp, ws_bytes, -1, sp),
+                    lambda: K.bagua_minmax_u8_decompress(dcode, cq, S, n, p, yq, sp)]
 
         def launches():
             return [lambda: K.bagua_minmax_u8_compress(dcode, xp, n, n, p, cp, S, wp, ws_bytes, -1, sp),
@@ -220,6 +231,30 @@ def bench_codec(args, onebit: bool = False):
         "encode_gib_s": round(esz * n / (sum(per[:-1]) * 1e-3) / GiB, 1),
         "decode_gib_s": round(esz * n / (per[-1] * 1e-3) / GiB, 1),
     }
+    # Side line: the same steps alternating between two buckets, so each step's bucket
+    # was last touched a whole other bucket ago (>= 2 x 256 MiB of traffic since: no
+    # Infinity-Cache reuse across steps, which the one-bucket loop may enjoy)
+    if not args.no_cold:
+        x2 = (torch.randn(n, device=dev, generator=g) * 1e-3).to(tdt)
+        y2, comp2 = torch.empty_like(y), torch.empty_like(comp)
+        calls2 = launches_for(x2.data_ptr(), y2.data_ptr(), comp2.data_ptr()) if launches_for else None
+        if calls2 is not None:
+            pairs = [calls, calls2]
+            for k in range(4):
+                for c in pairs[k % 2]:
+                    c()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k in range(args.steps):
+                for c in pairs[k % 2]:
+                    rc = c()
+                    if rc:
+                        raise RuntimeError(f"kernel launch failed: {N.STATUS.get(rc, rc)}")
+            torch.cuda.synchronize()
+            cms = (time.perf_counter() - t0) * 1e3 / args.steps
+            extra["two_bucket_alternating"] = {"ms_per_step": round(cms, 4),
+                                               "gib_s": round(esz * n / (cms * 1e-3) / GiB, 2)}
+        del x2, y2, comp2
     cfg = {"workload": ("onebit_sign_scale" if onebit else "minmax_uint8") +
            f"_encode_decode_{esz * n >> 20}MiB_{args.dtype}_bucket", "bucket_elements": n, "n_chunks": p,
            "compressed_bytes": S, "config_index": 3 if onebit else 2}
