@@ -41,6 +41,18 @@ class bagua_tensor_t(ctypes.Structure):
                 ("dtype", ctypes.c_int32), ("device_id", ctypes.c_int32)]
 
 
+class bagua_bucket_op_t(ctypes.Structure):
+    """include/bagua_core.h bagua_bucket_op_t"""
+    _fields_ = [("kind", ctypes.c_int32), ("average", ctypes.c_int32), ("compression", ctypes.c_int32),
+                ("fused", ctypes.c_int32), ("comm", ctypes.c_void_p), ("weight", bagua_tensor_t),
+                ("left_peer_weight", bagua_tensor_t), ("right_peer_weight", bagua_tensor_t),
+                ("callback", ctypes.c_void_p), ("user", ctypes.c_void_p)]
+
+
+BUCKET_OP_CENTRALIZED_LOW_PRECISION, BUCKET_OP_CENTRALIZED_FULL_PRECISION = 1, 2
+BUCKET_OP_DECENTRALIZED_LOW_PRECISION, BUCKET_OP_CALLBACK = 3, 4
+STATUS_INVALID_ARG = 1
+
 _T = ctypes.POINTER(bagua_tensor_t)
 _vp, _sz, _i32, _u64, _f32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64, ctypes.c_float
 _C = ctypes.c_void_p  # BaguaSingleCommunicatorC*
@@ -173,6 +185,21 @@ CORE_SIGNATURES = {
     "bagua_decentralized_low_precision_synchronous_unfused": (_i32, [_C, _T, _T, _T, _T, _i32]),
     "bagua_decentralized_low_precision_pipelined": (_i32, [_C, _T, _T, _T, _T, _i32, _i32]),
     "bagua_ring_exchange_plan": (_i32, [_i32, _i32, _i32, _i32, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_sz)]),
+    "bagua_bucket_create": (_vp, [ctypes.c_char_p, _T, ctypes.POINTER(ctypes.c_char_p), _i32, ctypes.POINTER(_i32)]),
+    "bagua_bucket_destroy": (None, [_vp]),
+    "bagua_bucket_append_op": (_i32, [_vp, ctypes.POINTER(bagua_bucket_op_t)]),
+    "bagua_bucket_clear_ops": (_i32, [_vp]),
+    "bagua_bucket_num_ops": (_i32, [_vp]),
+    "bagua_bucket_mark_tensor_ready": (_i32, [_vp, ctypes.c_char_p, _u64]),
+    "bagua_bucket_ready_for_comm": (_i32, [_vp]),
+    "bagua_bucket_reset_comm_ready": (_i32, [_vp]),
+    "bagua_bucket_execute": (_i32, [_vp, _u64]),
+    "bagua_comm_backend_create": (_vp, [_sz, _i32]),
+    "bagua_comm_backend_destroy": (None, [_vp]),
+    "bagua_comm_backend_register_ordered_buckets": (_i32, [_vp, ctypes.POINTER(_vp), _i32]),
+    "bagua_comm_backend_mark_communication_ready": (_i32, [_vp, ctypes.c_char_p, _u64]),
+    "bagua_comm_backend_wait_pending_comm_ops": (_i32, [_vp, ctypes.POINTER(_i32)]),
+    "bagua_comm_backend_failures": (_i32, [_vp]),
     "bagua_ring_exchange_ops": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),
 }
 

@@ -1,0 +1,404 @@
+// backend.cpp — native bucket + ordered-bucket scheduler.
+//
+// Replaces the reference's Rust scheduler (bagua-core-internal/src/lib.rs:
+// 125-338, BaguaCommBackend) and bucket (datatypes/mod.rs:1072-1267,
+// BaguaBucket):
+//   * register_ordered_buckets fixes the order (duplicate tensor names or
+//     pointers are refused, lib.rs:270-298);
+//   * mark_communication_ready(tensor, ready event) marks a tensor, and while
+//     the FRONT bucket is fully ready it is rotated to the back and scheduled on
+//     a bounded channel to one worker thread (lib.rs:300-319);
+//   * the worker makes the bucket's stream wait for every tensor's ready event,
+//     builds the communication tensor (in place when the tensors are back to
+//     back, else a pool buffer packed on the stream and copied back after the
+//     ops, datatypes/mod.rs:963-1070), runs the bucket's comm ops through the
+//     C ABI (comm_ops.cpp) and marks the item done (lib.rs:209-254);
+//   * wait_pending_comm_ops waits for every scheduled item (lib.rs:321-337);
+//   * a monitor logs an op that runs longer than 300 s (lib.rs:255-265; the
+//     reference panics the process, here the failure is logged and kept).
+// No Python on this path: the worker never takes the GIL unless a bucket
+// carries a Python callback op (python_ffi_op.rs), which ctypes runs with it.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "bagua_core.h"
+#include "comm_internal.hpp"
+#include "runtime_util.hpp"
+
+namespace {
+
+struct BucketTensor {
+    bagua_tensor_t t;
+    std::string name;
+};
+
+}  // namespace
+
+struct BaguaBucketC {
+    std::string name;
+    std::vector<BucketTensor> tensors;
+    std::vector<bagua_bucket_op_t> ops;
+    std::unordered_set<std::string> ready;  // tensor names marked ready (guarded by `mu`)
+    std::unordered_map<std::string, uint64_t> events;  // name -> ready event of the next execution
+    std::mutex mu;
+
+    bool ready_for_comm() {  // datatypes/mod.rs:1256-1266 (padding tensors count as ready)
+        std::lock_guard<std::mutex> g(mu);
+        for (const BucketTensor& t : tensors)
+            if (!ready.count(t.name) && t.name.rfind("bagua_padding_tensor", 0) != 0) return false;
+        return true;
+    }
+};
+
+namespace {
+
+using namespace bagua;
+
+bool contiguous(const BaguaBucketC* b) {
+    const size_t esz = bagua_dtype_bytes(b->tensors[0].t.dtype);
+    uint64_t cur = 0;
+    for (size_t i = 0; i < b->tensors.size(); ++i) {
+        const bagua_tensor_t& t = b->tensors[i].t;
+        if (i > 0 && t.ptr != cur) return false;
+        cur = t.ptr + t.num_elem_allocated * esz;
+    }
+    return true;
+}
+
+hipStream_t ops_stream(const std::vector<bagua_bucket_op_t>& ops) {
+    for (const bagua_bucket_op_t& op : ops)
+        if (op.comm) return op.comm->stream;
+    return nullptr;
+}
+
+int run_op(const bagua_bucket_op_t& op, const bagua_tensor_t* flat, const char* bucket_name) {
+    switch (op.kind) {
+        case BAGUA_BUCKET_OP_CENTRALIZED_LOW_PRECISION:
+            return op.fused ? bagua_centralized_low_precision_synchronous(op.comm, flat, op.average, op.compression)
+                            : bagua_centralized_low_precision_synchronous_unfused(op.comm, flat, op.average,
+                                                                                  op.compression);
+        case BAGUA_BUCKET_OP_CENTRALIZED_FULL_PRECISION:
+            return bagua_centralized_full_precision_synchronous(op.comm, flat, op.average);
+        case BAGUA_BUCKET_OP_DECENTRALIZED_LOW_PRECISION:
+            return bagua_decentralized_low_precision_synchronous(op.comm, flat, &op.weight, &op.left_peer_weight,
+                                                                 &op.right_peer_weight, op.compression);
+        case BAGUA_BUCKET_OP_CALLBACK:
+            if (op.callback) op.callback(op.user, bucket_name);  // python_ffi_op.rs: call with the bucket name
+            return BAGUA_OK;
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+// the ready events a bucket collected, consumed once (datatypes/mod.rs:969-980 zeroes them)
+std::vector<uint64_t> take_events(BaguaBucketC* b) {
+    std::lock_guard<std::mutex> g(b->mu);
+    std::vector<uint64_t> ev;
+    for (auto& kv : b->events)
+        if (kv.second) ev.push_back(kv.second);
+    b->events.clear();
+    return ev;
+}
+
+std::vector<bagua_bucket_op_t> copy_ops(BaguaBucketC* b) {
+    std::lock_guard<std::mutex> g(b->mu);
+    return b->ops;
+}
+
+// get_communication_tensor + ops + Drop (datatypes/mod.rs:963-1070) with the
+// events and ops the bucket had when it was scheduled (lib.rs:143-146 clones the ops)
+int execute_bucket(BaguaBucketC* b, const std::vector<uint64_t>& events, const std::vector<bagua_bucket_op_t>& ops,
+                   hipStream_t s) {
+    if (b->tensors.empty()) return BAGUA_ERR_INVALID_ARG;
+    const bagua_tensor_t& first = b->tensors[0].t;
+    DeviceGuard guard(first.device_id);
+    for (uint64_t ev : events)  // :969-980 the stream waits for every tensor's ready event
+        if (hipStreamWaitEvent(s, (hipEvent_t)(uintptr_t)ev, 0) != hipSuccess) return BAGUA_ERR_HIP;
+    if (ops.empty()) return BAGUA_OK;
+    const size_t esz = bagua_dtype_bytes(first.dtype);
+    uint64_t total_alloc = 0, total = 0;
+    for (const BucketTensor& t : b->tensors) {
+        total_alloc += t.t.num_elem_allocated;
+        total += t.t.num_elem;
+    }
+    int rc = BAGUA_OK;
+    if (contiguous(b)) {
+        const bagua_tensor_t flat{first.ptr, total_alloc, total_alloc, first.dtype, first.device_id};
+        for (const bagua_bucket_op_t& op : ops)
+            if ((rc = run_op(op, &flat, b->name.c_str())) != BAGUA_OK) break;
+        return rc;
+    }
+    // :999-1038 pack num_elements() of every tensor into a pool buffer on the stream
+    PoolBuffer buf;
+    if ((rc = buf.allocate(first.device_id, total_alloc * esz)) != BAGUA_OK) return rc;
+    uint8_t* dst = buf.as<uint8_t>();
+    for (const BucketTensor& t : b->tensors) {
+        const size_t bytes = t.t.num_elem * esz;
+        if (bytes && hipMemcpyAsync(dst, (const void*)(uintptr_t)t.t.ptr, bytes, hipMemcpyDeviceToDevice, s) !=
+                         hipSuccess)
+            return BAGUA_ERR_HIP;
+        dst += bytes;
+    }
+    const bagua_tensor_t flat{buf.ptr(), total, total_alloc, first.dtype, first.device_id};
+    for (const bagua_bucket_op_t& op : ops)
+        if ((rc = run_op(op, &flat, b->name.c_str())) != BAGUA_OK) break;
+    // :1043-1070 copy back, then wait for the stream (the buffer returns to the pool)
+    const uint8_t* src = buf.as<uint8_t>();
+    for (const BucketTensor& t : b->tensors) {
+        const size_t bytes = t.t.num_elem * esz;
+        if (rc == BAGUA_OK && bytes &&
+            hipMemcpyAsync((void*)(uintptr_t)t.t.ptr, src, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            rc = BAGUA_ERR_HIP;
+        src += bytes;
+    }
+    const hipError_t e = hipStreamSynchronize(s);
+    return rc != BAGUA_OK ? rc : (e == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP);
+}
+
+struct Scheduled {
+    BaguaBucketC* bucket = nullptr;
+    std::vector<uint64_t> events;          // ready events at scheduling time
+    std::vector<bagua_bucket_op_t> ops;    // the bucket's ops at scheduling time
+    bool done = false;
+    int status = BAGUA_OK;
+};
+
+}  // namespace
+
+struct BaguaCommBackendC {
+    int device = 0;
+    size_t cap = 1;
+    std::mutex mu;
+    std::condition_variable cv_work, cv_space, cv_done;
+    std::deque<BaguaBucketC*> ordered;
+    std::unordered_map<std::string, BaguaBucketC*> mapping;  // tensor name -> bucket
+    std::deque<std::shared_ptr<Scheduled>> channel;          // bounded by `cap`
+    std::deque<std::shared_ptr<Scheduled>> pending;          // scheduled, not yet waited for
+    std::shared_ptr<Scheduled> current;
+    std::chrono::steady_clock::time_point current_start;
+    std::vector<std::string> failures;
+    bool stop = false;
+    std::thread worker, monitor;
+
+    void work() {
+        (void)hipSetDevice(device);  // lib.rs:210-213
+        for (;;) {
+            std::shared_ptr<Scheduled> item;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv_work.wait(lk, [&] { return stop || !channel.empty(); });
+                if (channel.empty()) return;  // stopping with nothing queued
+                item = channel.front();
+                channel.pop_front();
+                cv_space.notify_all();
+                current = item;
+                current_start = std::chrono::steady_clock::now();
+            }
+            const int rc = execute_bucket(item->bucket, item->events, item->ops, ops_stream(item->ops));
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                item->status = rc;
+                item->done = true;
+                current.reset();
+            }
+            cv_done.notify_all();
+        }
+    }
+
+    void watch() {
+        std::unique_lock<std::mutex> lk(mu);
+        while (!stop) {
+            cv_work.wait_for(lk, std::chrono::seconds(5));
+            if (current && std::chrono::steady_clock::now() - current_start > std::chrono::seconds(300)) {
+                const std::string msg = "comm op on bucket " + current->bucket->name + " has not finished for 5 min";
+                bool seen = false;
+                for (const std::string& f : failures) seen = seen || f == msg;
+                if (!seen) {
+                    failures.push_back(msg);
+                    BAGUA_LOG(0, "%s", msg.c_str());
+                }
+            }
+        }
+    }
+};
+
+extern "C" {
+
+BaguaBucketC* bagua_bucket_create(const char* name, const bagua_tensor_t* tensors, const char* const* tensor_names,
+                                  int n, int* status) {
+    // datatypes/mod.rs:1079-1118 (same dtype and device; allocated >= num_elem)
+    int st = BAGUA_OK;
+    if (!name || !tensors || !tensor_names || n <= 0) st = BAGUA_ERR_INVALID_ARG;
+    for (int i = 0; st == BAGUA_OK && i < n; ++i) {
+        if (!tensor_names[i] || tensors[i].dtype != tensors[0].dtype || tensors[i].device_id != tensors[0].device_id ||
+            tensors[i].num_elem_allocated < tensors[i].num_elem || !bagua_dtype_bytes(tensors[i].dtype))
+            st = BAGUA_ERR_INVALID_ARG;
+    }
+    if (status) *status = st;
+    if (st != BAGUA_OK) return nullptr;
+    auto* b = new BaguaBucketC();
+    b->name = name;
+    for (int i = 0; i < n; ++i) b->tensors.push_back(BucketTensor{tensors[i], tensor_names[i]});
+    return b;
+}
+
+void bagua_bucket_destroy(BaguaBucketC* b) { delete b; }
+
+int bagua_bucket_append_op(BaguaBucketC* b, const bagua_bucket_op_t* op) {
+    if (!b || !op) return BAGUA_ERR_INVALID_ARG;
+    if (op->kind != BAGUA_BUCKET_OP_CALLBACK && !op->comm) return BAGUA_ERR_INVALID_ARG;
+    if (op->kind < BAGUA_BUCKET_OP_CENTRALIZED_LOW_PRECISION || op->kind > BAGUA_BUCKET_OP_CALLBACK)
+        return BAGUA_ERR_UNSUPPORTED;
+    std::lock_guard<std::mutex> g(b->mu);
+    b->ops.push_back(*op);
+    return BAGUA_OK;
+}
+
+int bagua_bucket_clear_ops(BaguaBucketC* b) {
+    if (!b) return BAGUA_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(b->mu);
+    b->ops.clear();
+    return BAGUA_OK;
+}
+
+int bagua_bucket_num_ops(BaguaBucketC* b) { return b ? (int)b->ops.size() : -1; }
+
+int bagua_bucket_mark_tensor_ready(BaguaBucketC* b, const char* tensor_name, uint64_t ready_event) {
+    if (!b || !tensor_name) return BAGUA_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(b->mu);
+    for (const BucketTensor& t : b->tensors)
+        if (t.name == tensor_name) {
+            b->ready.insert(t.name);
+            if (ready_event) b->events[t.name] = ready_event;
+            return BAGUA_OK;
+        }
+    return BAGUA_ERR_INVALID_ARG;
+}
+
+int bagua_bucket_ready_for_comm(BaguaBucketC* b) { return b && b->ready_for_comm() ? 1 : 0; }
+
+int bagua_bucket_reset_comm_ready(BaguaBucketC* b) {
+    if (!b) return BAGUA_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(b->mu);
+    b->ready.clear();
+    return BAGUA_OK;
+}
+
+int bagua_bucket_execute(BaguaBucketC* b, uint64_t stream) {
+    if (!b) return BAGUA_ERR_INVALID_ARG;
+    const std::vector<bagua_bucket_op_t> ops = copy_ops(b);
+    hipStream_t s = stream ? (hipStream_t)(uintptr_t)stream : ops_stream(ops);
+    return execute_bucket(b, take_events(b), ops, s);
+}
+
+BaguaCommBackendC* bagua_comm_backend_create(size_t schedule_channel_cap, int device_id) {
+    if (hipSetDevice(device_id) != hipSuccess) return nullptr;  // lib.rs:177-181
+    auto* be = new BaguaCommBackendC();
+    be->device = device_id;
+    be->cap = schedule_channel_cap ? schedule_channel_cap : 1;
+    be->worker = std::thread([be] { be->work(); });
+    be->monitor = std::thread([be] { be->watch(); });
+    return be;
+}
+
+void bagua_comm_backend_destroy(BaguaCommBackendC* be) {
+    if (!be) return;
+    {
+        std::lock_guard<std::mutex> lk(be->mu);
+        be->stop = true;
+    }
+    be->cv_work.notify_all();
+    be->cv_space.notify_all();
+    // the worker drains what is queued, then exits
+    if (be->worker.joinable()) be->worker.join();
+    if (be->monitor.joinable()) be->monitor.join();
+    delete be;
+}
+
+int bagua_comm_backend_wait_pending_comm_ops(BaguaCommBackendC* be, int* completed) {
+    // lib.rs:321-337: wait for every scheduled op; the first failure is returned
+    if (!be) return BAGUA_ERR_INVALID_ARG;
+    int n = 0, rc = BAGUA_OK;
+    std::unique_lock<std::mutex> lk(be->mu);
+    while (!be->pending.empty()) {
+        std::shared_ptr<Scheduled> item = be->pending.front();
+        be->pending.pop_front();
+        be->cv_done.wait(lk, [&] { return item->done; });
+        ++n;
+        if (rc == BAGUA_OK && item->status != BAGUA_OK) rc = item->status;
+    }
+    if (completed) *completed = n;
+    return rc;
+}
+
+int bagua_comm_backend_register_ordered_buckets(BaguaCommBackendC* be, BaguaBucketC* const* buckets, int n) {
+    // lib.rs:270-298: calling again replaces the previous buckets
+    if (!be || (n > 0 && !buckets)) return BAGUA_ERR_INVALID_ARG;
+    int done = 0;
+    const int rc = bagua_comm_backend_wait_pending_comm_ops(be, &done);
+    if (rc != BAGUA_OK) return rc;
+    std::unordered_map<std::string, BaguaBucketC*> mapping;
+    std::unordered_set<uint64_t> ptrs;
+    for (int i = 0; i < n; ++i) {
+        if (!buckets[i]) return BAGUA_ERR_INVALID_ARG;
+        for (const BucketTensor& t : buckets[i]->tensors) {
+            if (mapping.count(t.name) || ptrs.count(t.t.ptr)) {
+                BAGUA_LOG(0, "TensorError: duplicated tensor detected, name %s, ptr %llu", t.name.c_str(),
+                          (unsigned long long)t.t.ptr);
+                return BAGUA_ERR_INVALID_ARG;
+            }
+            mapping[t.name] = buckets[i];
+            ptrs.insert(t.t.ptr);
+        }
+    }
+    std::lock_guard<std::mutex> lk(be->mu);
+    be->mapping.swap(mapping);
+    be->ordered.assign(buckets, buckets + n);
+    return BAGUA_OK;
+}
+
+int bagua_comm_backend_mark_communication_ready(BaguaCommBackendC* be, const char* tensor_name, uint64_t ready_event) {
+    // lib.rs:300-319
+    if (!be || !tensor_name) return BAGUA_ERR_INVALID_ARG;
+    std::unique_lock<std::mutex> lk(be->mu);
+    if (be->ordered.empty()) return BAGUA_ERR_INVALID_ARG;  // "ordered buckets not yet set in comm backend"
+    auto it = be->mapping.find(tensor_name);
+    if (it == be->mapping.end()) return BAGUA_ERR_INVALID_ARG;
+    int rc = bagua_bucket_mark_tensor_ready(it->second, tensor_name, ready_event);
+    if (rc != BAGUA_OK) return rc;
+    while (be->ordered.front()->ready_for_comm()) {
+        BaguaBucketC* b = be->ordered.front();
+        be->ordered.pop_front();
+        bagua_bucket_reset_comm_ready(b);
+        be->ordered.push_back(b);
+        // bounded channel (flume::bounded(schedule_channel_cap)): wait for space
+        be->cv_space.wait(lk, [&] { return be->stop || be->channel.size() < be->cap; });
+        if (be->stop) return BAGUA_ERR_INVALID_ARG;
+        auto item = std::make_shared<Scheduled>();
+        item->bucket = b;
+        item->events = take_events(b);
+        item->ops = copy_ops(b);
+        be->channel.push_back(item);
+        be->pending.push_back(item);
+        be->cv_work.notify_all();
+    }
+    return BAGUA_OK;
+}
+
+int bagua_comm_backend_failures(BaguaCommBackendC* be) {
+    if (!be) return -1;
+    std::lock_guard<std::mutex> lk(be->mu);
+    return (int)be->failures.size();
+}
+
+}  // extern "C"

@@ -60,7 +60,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["auto", "codec", "allreduce", "onebit", "host"], default="auto")
+    ap.add_argument("--workload", choices=["auto", "codec", "allreduce", "onebit", "host", "backend"], default="auto")
+    ap.add_argument("--buckets", type=int, default=32, help="backend workload: gradient buckets per iteration")
+    ap.add_argument("--bucket-mib", type=int, default=25, help="backend workload: MiB of fp32 gradient per bucket")
     ap.add_argument("--elements", type=int, default=0, help="override bucket elements")
     ap.add_argument("--dtype", choices=["f32", "f16", "bf16"], default="f32",
                     help="codec workloads: gradient dtype (the headline is f32; bf16/f16 buckets keep 256 MiB)")
@@ -635,6 +637,73 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     return value, t_c * 1e3, roof, cfg, extra
 
 
+def bench_backend(args, world: int, rank: int, local_rank: int):
+    """The scheduler (BaguaCommBackendPy, bagua-core-internal/src/lib.rs:176-338)
+    driving a model-sized gradient: `--buckets` buckets of `--bucket-mib` MiB fp32
+    (4 tensors each, contiguous), each with the compressed centralized op.  One
+    iteration = every tensor marked ready in reverse bucket order (as backward
+    produces them, each with a ready event) + wait_pending_comm_ops.  value = GiB of
+    gradient per second (all ranks)."""
+    import torch.distributed as dist
+    import bagua_core
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    uid = [bagua_core.BaguaSingleCommunicatorPy.generate_nccl_unique_id_str() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0)
+    comm_stream = torch.cuda.Stream(device=dev)
+    comm = bagua_core.BaguaSingleCommunicatorPy(rank, world, local_rank, comm_stream.cuda_stream, uid[0])
+    per = (args.bucket_mib << 20) // 4
+    per -= per % (4 * 32 * world)
+    g = torch.Generator(device=dev).manual_seed(0x5EED + rank)
+    flats = [torch.randn(per, device=dev, generator=g) * 1e-3 for _ in range(args.buckets)]
+    buckets, tensors = [], []
+    for b, flat in enumerate(flats):
+        ts = [bagua_core.BaguaTensorPy(v, f"b{b}.t{i}") for i, v in enumerate(flat.view(4, -1).unbind(0))]
+        bk = bagua_core.BaguaBucketPy(f"bucket{b}", ts)
+        bk.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+        buckets.append(bk)
+        tensors.append(ts)
+    backend = bagua_core.BaguaCommBackendPy(args.buckets, local_rank)
+    # backward produces the last layers' gradients first: the registration order is the
+    # order buckets become ready
+    backend.register_ordered_buckets(list(reversed(buckets)))
+    events = [torch.cuda.Event() for _ in range(args.buckets)]
+
+    def iteration():
+        for b in reversed(range(args.buckets)):
+            events[b].record()
+            for t in tensors[b]:
+                backend.mark_communication_ready(t, events[b].cuda_event)
+        done = backend.wait_pending_comm_ops()
+        assert done == args.buckets, done
+
+    for _ in range(max(1, args.warmup)):
+        iteration()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        iteration()
+    torch.cuda.synchronize()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.barrier()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = float(t.item()) / args.steps * 1e3
+    grad_bytes = 4.0 * per * args.buckets
+    value = world * grad_bytes / (ms * 1e-3) / GiB
+    cfg = {"workload": f"comm_backend_{args.buckets}x{args.bucket_mib}MiB_fp32_buckets_minmax_uint8",
+           "bucket_elements": per, "buckets": args.buckets, "tensors_per_bucket": 4,
+           "parallelism": f"dp{world}", "scheduler": type(backend).__module__ + "." + type(backend).__name__}
+    extra = {"per_bucket_us": round(ms * 1e3 / args.buckets, 2), "per_rank_gib_s": round(value / world, 2)}
+    del backend, buckets, comm
+    return value, ms, None, cfg, extra
+
+
 def _finite(o):
     """NaN / inf (a failed side measurement) -> null: the line stays strict JSON."""
     if isinstance(o, float):
@@ -669,6 +738,9 @@ def main():
         dtype = f"{args.dtype} -> u8" if workload == "codec" else f"{args.dtype} -> 1bit"
     elif workload == "host":
         value, ms, roof, cfg, extra = bench_host(args)
+        dtype = "f32 -> u8"
+    elif workload == "backend":
+        value, ms, roof, cfg, extra = bench_backend(args, world, rank, local_rank)
         dtype = "f32 -> u8"
     else:
         value, ms, roof, cfg, extra = bench_allreduce(args, world, rank, local_rank)

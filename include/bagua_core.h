@@ -198,6 +198,63 @@ int bagua_decentralized_low_precision_synchronous_unfused(BaguaSingleCommunicato
                                                           const bagua_tensor_t* left_peer_weight,
                                                           const bagua_tensor_t* right_peer_weight, int method);
 
+/* ------------------------------------------------------ bucket + scheduler -- */
+/* BaguaBucket (datatypes/mod.rs:1072-1267) and BaguaCommBackend (src/lib.rs:125-338)
+ * in C++: a bucket is a named list of tensors (same dtype and device) plus comm
+ * ops; the backend schedules buckets in registration order as their tensors are
+ * marked ready and runs their ops on one native worker thread. */
+typedef struct BaguaBucketC BaguaBucketC;
+typedef struct BaguaCommBackendC BaguaCommBackendC;
+
+enum {
+    BAGUA_BUCKET_OP_CENTRALIZED_LOW_PRECISION = 1,   /* centralized_low_precision_synchronous.rs */
+    BAGUA_BUCKET_OP_CENTRALIZED_FULL_PRECISION = 2,  /* centralized_full_precision_synchronous.rs */
+    BAGUA_BUCKET_OP_DECENTRALIZED_LOW_PRECISION = 3, /* decentralized_low_precision_synchronous.rs */
+    BAGUA_BUCKET_OP_CALLBACK = 4                     /* python_ffi_op.rs: callback(user, bucket name) */
+};
+
+typedef struct bagua_bucket_op {
+    int32_t kind;
+    int32_t average;     /* centralized ops */
+    int32_t compression; /* BAGUA_COMPRESSION_* (low-precision ops) */
+    int32_t fused;       /* centralized low precision: 1 = fused / pipelined, 0 = the reference's sequence */
+    BaguaSingleCommunicatorC* comm;
+    bagua_tensor_t weight, left_peer_weight, right_peer_weight; /* decentralized op */
+    void (*callback)(void* user, const char* bucket_name);     /* BAGUA_BUCKET_OP_CALLBACK */
+    void* user;
+} bagua_bucket_op_t;
+
+/* NULL on error (*status says why): empty list, mixed dtype / device, allocated < num_elem */
+BaguaBucketC* bagua_bucket_create(const char* name, const bagua_tensor_t* tensors, const char* const* tensor_names,
+                                  int n, int* status);
+void bagua_bucket_destroy(BaguaBucketC* bucket);
+int bagua_bucket_append_op(BaguaBucketC* bucket, const bagua_bucket_op_t* op);
+int bagua_bucket_clear_ops(BaguaBucketC* bucket);
+int bagua_bucket_num_ops(BaguaBucketC* bucket);
+/* readiness by tensor name (datatypes/mod.rs:793-813, 1256-1266); the event (0 = none)
+ * is waited for by the stream of the bucket's next execution */
+int bagua_bucket_mark_tensor_ready(BaguaBucketC* bucket, const char* tensor_name, uint64_t ready_event);
+int bagua_bucket_ready_for_comm(BaguaBucketC* bucket);
+int bagua_bucket_reset_comm_ready(BaguaBucketC* bucket);
+/* run the bucket's ops now on its communication tensor (in place when the tensors are
+ * back to back, else packed into a pool buffer and copied back, datatypes/mod.rs:963-1070);
+ * stream 0 = the first op's communicator stream.  Synchronous. */
+int bagua_bucket_execute(BaguaBucketC* bucket, uint64_t stream);
+
+BaguaCommBackendC* bagua_comm_backend_create(size_t schedule_channel_cap, int device_id);
+/* drains what is already scheduled, then stops the worker */
+void bagua_comm_backend_destroy(BaguaCommBackendC* backend);
+/* lib.rs:270-298: replaces the previous buckets; duplicate tensor names or pointers are
+ * refused.  The buckets must outlive their registration. */
+int bagua_comm_backend_register_ordered_buckets(BaguaCommBackendC* backend, BaguaBucketC* const* buckets, int n);
+/* lib.rs:300-319 (the tensor by name) */
+int bagua_comm_backend_mark_communication_ready(BaguaCommBackendC* backend, const char* tensor_name,
+                                               uint64_t ready_event);
+/* lib.rs:321-337: *completed = ops waited for; returns the first failure's status */
+int bagua_comm_backend_wait_pending_comm_ops(BaguaCommBackendC* backend, int* completed);
+/* ops the monitor saw running longer than 300 s (lib.rs:255-265) */
+int bagua_comm_backend_failures(BaguaCommBackendC* backend);
+
 #ifdef __cplusplus
 }
 #endif

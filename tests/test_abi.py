@@ -31,7 +31,7 @@ def declared(header: str) -> list[str]:
     src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     names = re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", src)
-    skip = {"if", "for", "while", "return", "sizeof"}
+    skip = {"if", "for", "while", "return", "sizeof", "void"}  # "void (*callback)(...)" is a field
     return sorted({n for n in names if n not in skip})
 
 

@@ -1,0 +1,177 @@
+"""GPU tests of the native bucket + scheduler (csrc/runtime/backend.cpp), the
+reference's BaguaCommBackend (bagua-core-internal/src/lib.rs:125-338) and
+BaguaBucket (datatypes/mod.rs:1072-1267) semantics:
+
+* buckets are scheduled in registration order, each as soon as it and every
+  bucket before it are fully ready (lib.rs:300-319), and run on one worker;
+* the worker waits for the tensors' ready events on the communicator stream;
+* a Python op is called with the bucket's name (python_ffi_op.rs);
+* a bounded channel (capacity 1) still schedules every bucket;
+* an op failure surfaces from wait_pending_comm_ops;
+* results equal the oracle simulation of the reference op sequence, for
+  contiguous buckets (in place) and scattered ones (packed + copied back).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import simulate
+
+pytestmark = pytest.mark.gpu
+
+F32 = 0
+
+
+@pytest.fixture(scope="module")
+def bc():
+    import bagua_core
+    return bagua_core
+
+
+@pytest.fixture(scope="module")
+def comm(bc):
+    stream = torch.cuda.Stream()
+    uid = bc.BaguaSingleCommunicatorPy.generate_nccl_unique_id_str()
+    c = bc.BaguaSingleCommunicatorPy(0, 1, 0, stream.cuda_stream, uid)
+    c._keep_stream = stream
+    return c
+
+
+def _grads(n_buckets, per, seed, scattered=False):
+    rng = np.random.default_rng(seed)
+    host = [(rng.standard_normal(per) * 1e-3).astype(np.float32) for _ in range(n_buckets)]
+    if scattered:  # every tensor its own allocation, with gaps between them
+        devs, keep = [], []
+        for h in host:
+            parts = []
+            for q in np.array_split(h, 3):
+                parts.append(torch.from_numpy(q.copy()).cuda())
+                keep.append(torch.empty(4096, device="cuda"))
+            devs.append(parts)
+        return host, devs, keep
+    flats = [torch.from_numpy(h.copy()).cuda() for h in host]
+    return host, [list(f.view(3, -1).unbind(0)) if per % 3 == 0 else [f] for f in flats], flats
+
+
+@pytest.mark.parametrize("scattered", [False, True])
+def test_scheduler_runs_buckets_in_order_and_matches_oracle(bc, comm, oracle_c, scattered):
+    n_buckets, per = 6, 3 * 40000
+    host, parts, _keep = _grads(n_buckets, per, 7 + scattered, scattered)
+    log = []
+    buckets, tensors = [], []
+    for b in range(n_buckets):
+        ts = [bc.BaguaTensorPy(t, f"g{b}.{i}") for i, t in enumerate(parts[b])]
+        bk = bc.BaguaBucketPy(f"bucket{b}", ts)
+        bk.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+        bk.append_python_op(lambda name: log.append(name))
+        buckets.append(bk)
+        tensors.append(ts)
+    backend = bc.BaguaCommBackendPy(2, 0)
+    backend.register_ordered_buckets(buckets)
+    ev = torch.cuda.Event()
+    # mark the LAST bucket first: nothing may run until bucket 0 is ready
+    for t in tensors[-1]:
+        backend.mark_communication_ready(t, 0)
+    assert backend.wait_pending_comm_ops() == 0
+    for b in range(n_buckets - 1):
+        ev.record()
+        for t in tensors[b]:
+            backend.mark_communication_ready(t, ev.cuda_event)
+    assert backend.wait_pending_comm_ops() == n_buckets
+    assert log == [f"bucket{b}" for b in range(n_buckets)], log  # registration order, bucket name passed
+    for b in range(n_buckets):
+        want = simulate.centralized_low_precision(oracle_c, [host[b]], F32, True)[0]
+        got = torch.cat([t.reshape(-1) for t in parts[b]]).cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"bucket {b}"
+
+
+def test_bounded_channel_capacity_one(bc, comm):
+    """capacity 1: scheduling a bucket waits for channel space, never drops one"""
+    n_buckets = 12
+    flats = [torch.randn(3 * 4096, device="cuda") * 1e-3 for _ in range(n_buckets)]
+    seen = []
+    buckets = []
+    for b, f in enumerate(flats):
+        bk = bc.BaguaBucketPy(f"b{b}", [bc.BaguaTensorPy(f, f"t{b}")])
+        bk.append_python_op(lambda name: seen.append(name))
+        buckets.append(bk)
+    backend = bc.BaguaCommBackendPy(1, 0)
+    backend.register_ordered_buckets(buckets)
+    for it in range(3):
+        for b in range(n_buckets):
+            backend.mark_communication_ready(buckets[b].tensors()[0], 0)
+        assert backend.wait_pending_comm_ops() == n_buckets
+    assert seen == [f"b{b}" for b in range(n_buckets)] * 3
+
+
+def test_ready_event_orders_the_comm_stream(bc, comm, oracle_c):
+    """The gradient is written on the compute stream AFTER a long sleep; the event
+    recorded behind that write must hold the comm op back (datatypes/mod.rs:969-980)."""
+    n = 3 * 50000
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+    t = torch.zeros(n, device="cuda")
+    bt = bc.BaguaTensorPy(t, "late")
+    bk = bc.BaguaBucketPy("late_bucket", [bt])
+    bk.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+    backend = bc.BaguaCommBackendPy(4, 0)
+    backend.register_ordered_buckets([bk])
+    src = torch.from_numpy(x).cuda()
+    torch.cuda.synchronize()
+    torch.cuda._sleep(100_000_000)
+    t.copy_(src)
+    ev = torch.cuda.Event()
+    ev.record()
+    backend.mark_communication_ready(bt, ev.cuda_event)
+    assert backend.wait_pending_comm_ops() == 1
+    want = simulate.centralized_low_precision(oracle_c, [x], F32, True)[0]
+    assert np.array_equal(t.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+def test_op_failure_surfaces(bc):
+    """An op that fails (an aborted communicator) is reported by wait_pending_comm_ops."""
+    from bagua_core.communicator import loopback_communicators
+    comms = loopback_communicators(1, 0)
+    comms[0].abort()
+    f = torch.randn(3 * 1024, device="cuda")
+    bk = bc.BaguaBucketPy("doomed", [bc.BaguaTensorPy(f, "d")])
+    bk.append_centralized_synchronous_op(comms[0], None, False, True, False, "MinMaxUInt8")
+    backend = bc.BaguaCommBackendPy(2, 0)
+    backend.register_ordered_buckets([bk])
+    backend.mark_communication_ready(bk.tensors()[0], 0)
+    with pytest.raises(RuntimeError, match="comm op failed"):
+        backend.wait_pending_comm_ops()
+
+
+def test_registration_errors(bc, comm):
+    f = torch.randn(4096, device="cuda")
+    a = bc.BaguaTensorPy(f, "x")
+    bk1 = bc.BaguaBucketPy("b1", [a])
+    backend = bc.BaguaCommBackendPy(2, 0)
+    with pytest.raises(RuntimeError, match="ordered buckets not yet set"):
+        backend.mark_communication_ready(a, 0)
+    with pytest.raises(RuntimeError, match="duplicated tensor"):
+        backend.register_ordered_buckets([bk1, bc.BaguaBucketPy("b2", [bc.BaguaTensorPy(f, "x")])])
+    backend.register_ordered_buckets([bk1])
+    with pytest.raises(RuntimeError, match="not registered"):
+        backend.mark_communication_ready(bc.BaguaTensorPy(torch.randn(8, device="cuda"), "y"), 0)
+    with pytest.raises(RuntimeError):
+        bc.BaguaBucketPy("mixed", [a, bc.BaguaTensorPy(torch.randn(8, device="cuda", dtype=torch.float16), "h")])
+
+
+def test_bucket_readiness_api(bc, comm):
+    """BaguaBucketPy.ready_for_comm / reset_comm_ready (lib.rs:479-486); padding tensors
+    (name prefix bagua_padding_tensor) count as ready."""
+    f = torch.randn(3 * 1024, device="cuda")
+    ts = [bc.BaguaTensorPy(v, n) for v, n in zip(f.view(3, -1).unbind(0), ["a", "b", "bagua_padding_tensor_0"])]
+    bk = bc.BaguaBucketPy("r", ts)
+    assert not bk.ready_for_comm()
+    bk.mark_tensor_ready(ts[0])
+    assert not bk.ready_for_comm()
+    bk.mark_tensor_ready(ts[1])
+    assert bk.ready_for_comm()
+    bk.reset_comm_ready()
+    assert not bk.ready_for_comm()
+    assert ctypes.c_int(bc._native.C.bagua_bucket_num_ops(bk.handle)).value == 0

@@ -69,8 +69,8 @@ def test_centralized_low_precision_p1(bc, comm, oracle_c, dtype, fused):
     want = simulate.centralized_low_precision(oracle_c, [x], dtype, True)[0]
     t = dev(x, dtype)
     b = bc.BaguaBucketPy("b", [bc.BaguaTensorPy(t, "t")])
-    b.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
-    b._ops[0].fused = fused
+    from bagua_core.bucket import CentralizedLowPrecisionSynchronous
+    b._append(CentralizedLowPrecisionSynchronous(comm, True, "MinMaxUInt8", fused))
     b.execute_ops()
     assert np.array_equal(host(t, dtype).view(np.uint8), want.view(np.uint8))
 
