@@ -174,6 +174,7 @@ CORE_SIGNATURES = {
     "bagua_comm_group_end": (_i32, []),
     "bagua_comm_barrier": (_i32, [_C]),
     "bagua_comm_synchronize": (_i32, [_C]),
+    "bagua_comm_set_async": (_i32, [_C, _i32]),
     "bagua_loopback_group_create": (_vp, [_i32, _i32]),
     "bagua_loopback_group_destroy": (None, [_vp]),
     "bagua_loopback_communicator_create": (_C, [_vp, _sz, _u64]),

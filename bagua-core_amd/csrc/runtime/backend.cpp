@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -82,7 +83,7 @@ hipStream_t ops_stream(const std::vector<bagua_bucket_op_t>& ops) {
     return nullptr;
 }
 
-int run_op(const bagua_bucket_op_t& op, const bagua_tensor_t* flat, const char* bucket_name) {
+int run_op(const bagua_bucket_op_t& op, const bagua_tensor_t* flat, const char* bucket_name, hipStream_t s) {
     switch (op.kind) {
         case BAGUA_BUCKET_OP_CENTRALIZED_LOW_PRECISION:
             return op.fused ? bagua_centralized_low_precision_synchronous(op.comm, flat, op.average, op.compression)
@@ -94,6 +95,9 @@ int run_op(const bagua_bucket_op_t& op, const bagua_tensor_t* flat, const char* 
             return bagua_decentralized_low_precision_synchronous(op.comm, flat, &op.weight, &op.left_peer_weight,
                                                                  &op.right_peer_weight, op.compression);
         case BAGUA_BUCKET_OP_CALLBACK:
+            // the callback sees the previous ops' results, as in the reference (their
+            // Drop synced), also when the worker runs the ops async
+            if (g_async_ops && hipStreamSynchronize(s) != hipSuccess) return BAGUA_ERR_HIP;
             if (op.callback) op.callback(op.user, bucket_name);  // python_ffi_op.rs: call with the bucket name
             return BAGUA_OK;
     }
@@ -135,7 +139,7 @@ int execute_bucket(BaguaBucketC* b, const std::vector<uint64_t>& events, const s
     if (contiguous(b)) {
         const bagua_tensor_t flat{first.ptr, total_alloc, total_alloc, first.dtype, first.device_id};
         for (const bagua_bucket_op_t& op : ops)
-            if ((rc = run_op(op, &flat, b->name.c_str())) != BAGUA_OK) break;
+            if ((rc = run_op(op, &flat, b->name.c_str(), s)) != BAGUA_OK) break;
         return rc;
     }
     // :999-1038 pack num_elements() of every tensor into a pool buffer on the stream
@@ -151,8 +155,9 @@ int execute_bucket(BaguaBucketC* b, const std::vector<uint64_t>& events, const s
     }
     const bagua_tensor_t flat{buf.ptr(), total, total_alloc, first.dtype, first.device_id};
     for (const bagua_bucket_op_t& op : ops)
-        if ((rc = run_op(op, &flat, b->name.c_str())) != BAGUA_OK) break;
-    // :1043-1070 copy back, then wait for the stream (the buffer returns to the pool)
+        if ((rc = run_op(op, &flat, b->name.c_str(), s)) != BAGUA_OK) break;
+    // :1043-1070 copy back, then wait for the stream (the buffer returns to the pool);
+    // async: the buffer returns to the pool behind the stream instead
     const uint8_t* src = buf.as<uint8_t>();
     for (const BucketTensor& t : b->tensors) {
         const size_t bytes = t.t.num_elem * esz;
@@ -160,6 +165,13 @@ int execute_bucket(BaguaBucketC* b, const std::vector<uint64_t>& events, const s
             hipMemcpyAsync((void*)(uintptr_t)t.t.ptr, src, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
             rc = BAGUA_ERR_HIP;
         src += bytes;
+    }
+    if (g_async_ops) {
+        const uint64_t sv = (uint64_t)(uintptr_t)s;
+        const uint64_t p = buf.ptr();
+        buf.release_to_caller();
+        (void)pool_free_after(p, &sv, 1);
+        return rc;
     }
     const hipError_t e = hipStreamSynchronize(s);
     return rc != BAGUA_OK ? rc : (e == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP);
@@ -169,8 +181,9 @@ struct Scheduled {
     BaguaBucketC* bucket = nullptr;
     std::vector<uint64_t> events;          // ready events at scheduling time
     std::vector<bagua_bucket_op_t> ops;    // the bucket's ops at scheduling time
-    bool done = false;
+    bool done = false;                     // executed (sync) / enqueued (async)
     int status = BAGUA_OK;
+    hipEvent_t finished = nullptr;         // async: recorded behind the bucket's work
 };
 
 }  // namespace
@@ -188,10 +201,27 @@ struct BaguaCommBackendC {
     std::chrono::steady_clock::time_point current_start;
     std::vector<std::string> failures;
     bool stop = false;
+    bool async = true;                  // BAGUA_BACKEND_SYNC=1: every op waits for its stream
+    std::vector<hipEvent_t> spare;      // completion events for reuse
     std::thread worker, monitor;
+
+    hipEvent_t take_event() {  // caller holds mu
+        if (!spare.empty()) {
+            hipEvent_t e = spare.back();
+            spare.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        // completion only: no system-scope fence (profiles/r02_slot_event_ab.jsonl)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) return nullptr;
+        return e;
+    }
 
     void work() {
         (void)hipSetDevice(device);  // lib.rs:210-213
+        // async: ops return once enqueued; buckets run back to back on the stream and
+        // wait_pending_comm_ops waits for each bucket's completion event
+        g_async_ops = async;
         for (;;) {
             std::shared_ptr<Scheduled> item;
             {
@@ -204,10 +234,21 @@ struct BaguaCommBackendC {
                 current = item;
                 current_start = std::chrono::steady_clock::now();
             }
-            const int rc = execute_bucket(item->bucket, item->events, item->ops, ops_stream(item->ops));
+            hipStream_t s = ops_stream(item->ops);
+            const int rc = execute_bucket(item->bucket, item->events, item->ops, s);
+            hipEvent_t fin = nullptr;
+            if (async && rc == BAGUA_OK) {
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    fin = take_event();
+                }
+                if (fin && hipEventRecord(fin, s) != hipSuccess) fin = nullptr;
+            }
             {
                 std::lock_guard<std::mutex> lk(mu);
                 item->status = rc;
+                item->finished = fin;
+                if (async && rc == BAGUA_OK && !fin) item->status = BAGUA_ERR_HIP;
                 item->done = true;
                 current.reset();
             }
@@ -305,6 +346,8 @@ BaguaCommBackendC* bagua_comm_backend_create(size_t schedule_channel_cap, int de
     if (hipSetDevice(device_id) != hipSuccess) return nullptr;  // lib.rs:177-181
     auto* be = new BaguaCommBackendC();
     be->device = device_id;
+    const char* sync = std::getenv("BAGUA_BACKEND_SYNC");
+    be->async = !(sync && *sync && std::atoi(sync) != 0);
     be->cap = schedule_channel_cap ? schedule_channel_cap : 1;
     be->worker = std::thread([be] { be->work(); });
     be->monitor = std::thread([be] { be->watch(); });
@@ -319,9 +362,12 @@ void bagua_comm_backend_destroy(BaguaCommBackendC* be) {
     }
     be->cv_work.notify_all();
     be->cv_space.notify_all();
-    // the worker drains what is queued, then exits
+    // the worker drains what is queued, then exits; enqueued work is waited for
     if (be->worker.joinable()) be->worker.join();
     if (be->monitor.joinable()) be->monitor.join();
+    int n = 0;
+    (void)bagua_comm_backend_wait_pending_comm_ops(be, &n);
+    for (hipEvent_t e : be->spare) (void)hipEventDestroy(e);
     delete be;
 }
 
@@ -334,6 +380,14 @@ int bagua_comm_backend_wait_pending_comm_ops(BaguaCommBackendC* be, int* complet
         std::shared_ptr<Scheduled> item = be->pending.front();
         be->pending.pop_front();
         be->cv_done.wait(lk, [&] { return item->done; });
+        if (item->finished) {  // async: the bucket's work has to complete, not just be enqueued
+            lk.unlock();
+            const hipError_t e = hipEventSynchronize(item->finished);
+            lk.lock();
+            if (e != hipSuccess && item->status == BAGUA_OK) item->status = BAGUA_ERR_HIP;
+            be->spare.push_back(item->finished);
+            item->finished = nullptr;
+        }
         ++n;
         if (rc == BAGUA_OK && item->status != BAGUA_OK) rc = item->status;
     }

@@ -39,6 +39,9 @@ Transport* make_rccl_transport(ncclComm_t comm);
 ncclDataType_t nccl_dtype(int d);
 int nccl_status(ncclResult_t r);
 
+// set by the native scheduler's worker thread: comm ops it runs are async
+extern thread_local bool g_async_ops;
+
 }  // namespace bagua
 
 struct BaguaSingleCommunicatorC {
@@ -52,6 +55,10 @@ struct BaguaSingleCommunicatorC {
     // runs the codec on piece k+1, and the events that order the two (lazy)
     hipStream_t side = nullptr;
     std::vector<hipEvent_t> events;
+    hipEvent_t join = nullptr;  // async ops: the side stream's end, waited for by `stream`
+    // async ops (bagua_comm_set_async, or the native scheduler's worker): an op returns
+    // once its work is enqueued; buffers go back to the pool behind the stream
+    bool async = false;
 
     int ensure_side(size_t n_events) {
         if (!side && hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) {
@@ -71,6 +78,10 @@ struct BaguaSingleCommunicatorC {
             if (hipEventCreateWithFlags(&e, flags) != hipSuccess) return -1;
             events.push_back(e);
         }
+        if (!join && hipEventCreateWithFlags(&join, flags) != hipSuccess) {
+            join = nullptr;
+            return -1;
+        }
         return 0;
     }
     ~BaguaSingleCommunicatorC() {
@@ -83,6 +94,11 @@ struct BaguaSingleCommunicatorC {
             if (side) (void)bagua_release_stream_resources(device_id, (uint64_t)(uintptr_t)side);
         }
         for (hipEvent_t e : events) (void)hipEventDestroy(e);
+        if (join) (void)hipEventDestroy(join);
         if (side) (void)hipStreamDestroy(side);
     }
 };
+
+namespace bagua {
+inline bool async_ops(const BaguaSingleCommunicatorC* c) { return c->async || g_async_ops; }
+}  // namespace bagua

@@ -31,6 +31,10 @@
 
 using namespace bagua;
 
+namespace bagua {
+thread_local bool g_async_ops = false;
+}
+
 namespace {
 
 struct Chunking {
@@ -61,11 +65,46 @@ bagua_tensor_t u8_view(uint64_t ptr, size_t bytes, int device) {
     return v;
 }
 
+// end of an op: wait for its stream (the reference syncs in
+// BaguaCommunicationTensor::drop, datatypes/mod.rs:1062-1066), or, async, return
+// with the work enqueued (OpBuffers then go back to the pool behind the stream)
 int finish(BaguaSingleCommunicatorC* c, int rc) {
+    if (async_ops(c)) return rc;
     const hipError_t e = hipStreamSynchronize(c->stream);
     if (rc) return rc;
     return e == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP;
 }
+
+// a pool buffer of one op: freed after the op's stream sync, or (async) behind the
+// op's stream, which the side stream has joined by then (finish_both)
+class OpBuffer {
+   public:
+    explicit OpBuffer(BaguaSingleCommunicatorC* c) : c_(c) {}
+    OpBuffer(const OpBuffer&) = delete;
+    OpBuffer& operator=(const OpBuffer&) = delete;
+    ~OpBuffer() { release(); }
+    int allocate(int device, size_t bytes) {
+        release();
+        return pool_alloc(device, bytes, &ptr_);
+    }
+    void release() {
+        if (!ptr_) return;
+        if (async_ops(c_)) {
+            const uint64_t s = (uint64_t)(uintptr_t)c_->stream;
+            (void)pool_free_after(ptr_, &s, 1);
+        } else {
+            (void)pool_free(ptr_);
+        }
+        ptr_ = 0;
+    }
+    uint64_t ptr() const { return ptr_; }
+    template <typename P>
+    P* as() const { return reinterpret_cast<P*>((uintptr_t)ptr_); }
+
+   private:
+    BaguaSingleCommunicatorC* c_;
+    uint64_t ptr_ = 0;
+};
 
 #define TRY(x)                 \
     do {                       \
@@ -79,7 +118,7 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
     if (rc) return rc;
     DeviceGuard guard(c->device_id);
     const uint64_t s = (uint64_t)(uintptr_t)c->stream;
-    PoolBuffer send, recv;
+    OpBuffer send(c), recv(c);
     TRY(send.allocate(c->device_id, k.S));
     TRY(recv.allocate(c->device_id, k.S));
     const bagua_tensor_t sv = u8_view(send.ptr(), k.S, c->device_id);
@@ -209,6 +248,12 @@ int exchange_piece(BaguaSingleCommunicatorC* c, const Chunking& k, uint8_t* send
 }
 
 int finish_both(BaguaSingleCommunicatorC* c, int rc) {
+    if (async_ops(c)) {
+        // the op's stream takes over the side stream's tail: its completion is the op's
+        if (hipEventRecord(c->join, c->side) != hipSuccess || hipStreamWaitEvent(c->stream, c->join, 0) != hipSuccess)
+            return rc ? rc : BAGUA_ERR_HIP;
+        return rc;
+    }
     const hipError_t e1 = hipStreamSynchronize(c->side);
     const int r0 = finish(c, rc);
     if (r0) return r0;
@@ -237,7 +282,7 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
     hipEvent_t requantised = gathered[pieces];
     const int dt = t->dtype, cs = (int)k.cs, p = k.p;
     void* x = (void*)(uintptr_t)t->ptr;
-    PoolBuffer send, recv;
+    OpBuffer send(c), recv(c);
     TRY(send.allocate(c->device_id, k.S));
     TRY(recv.allocate(c->device_id, k.S));
     uint8_t* sb = send.as<uint8_t>();
@@ -314,7 +359,7 @@ int centralized_pipelined_onebit(BaguaSingleCommunicatorC* c, const bagua_tensor
     hipEvent_t exchanged = gathered[pieces], requantised = gathered[pieces + 1];
     const int dt = t->dtype, cs = (int)k.cs, p = k.p;
     void* x = (void*)(uintptr_t)t->ptr;
-    PoolBuffer send, recv;
+    OpBuffer send(c), recv(c);
     TRY(send.allocate(c->device_id, k.S));
     TRY(recv.allocate(c->device_id, k.S));
     uint8_t* sb = send.as<uint8_t>();
@@ -549,7 +594,7 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
     const int n = (int)t->num_elem_allocated;
     const size_t S = bagua_compressed_size(method, t->dtype, 1, t->num_elem_allocated);
     if (!S) return BAGUA_ERR_UNSUPPORTED;
-    PoolBuffer mine, lbuf, rbuf;
+    OpBuffer mine(c), lbuf(c), rbuf(c);
     TRY(mine.allocate(c->device_id, S));
     TRY(lbuf.allocate(c->device_id, S));
     TRY(rbuf.allocate(c->device_id, S));
@@ -582,7 +627,7 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
                 RingPlan plan;
                 TRY(ring_plan((int)c->nranks, (int)c->rank, n, pieces, multipath, &plan));
                 if (plan.k.S != S) return finish(c, BAGUA_ERR_INVALID_ARG);
-                PoolBuffer relay;
+                OpBuffer relay(c);
                 if (ring_relay_bytes(plan)) TRY(relay.allocate(c->device_id, ring_relay_bytes(plan)));
                 if (c->ensure_side(2 * (size_t)pieces + 1)) return finish(c, BAGUA_ERR_HIP);
                 hipStream_t s1 = c->side;
@@ -656,6 +701,12 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
     TRY(bagua_tensor_add_inplace(t, weight, s));
     TRY(bagua_tensor_clone_from(weight, t, s));
     return finish(c, BAGUA_OK);
+}
+
+int bagua_comm_set_async(BaguaSingleCommunicatorC* c, int on) {
+    if (!c) return BAGUA_ERR_INVALID_ARG;
+    c->async = on != 0;
+    return BAGUA_OK;
 }
 
 int bagua_ring_exchange_plan(int nranks, int rank, int chunk_size, int pieces, int multipath, int* groups,

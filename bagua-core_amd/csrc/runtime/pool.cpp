@@ -157,7 +157,8 @@ int pool_free_after(uint64_t ptr, const uint64_t* streams, int n) {
         if (!d.spare_events.empty()) {
             e = d.spare_events.back();
             d.spare_events.pop_back();
-        } else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        } else if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+            // completion only (the block is reused on this device): no system-scope fence
             (void)hipGetLastError();
             e = nullptr;
         }

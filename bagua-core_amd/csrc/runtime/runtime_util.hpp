@@ -62,6 +62,8 @@ class PoolBuffer {
     }
     uint64_t ptr() const { return ptr_; }
     size_t bytes() const { return bytes_; }
+    // the caller takes over the block (e.g. to free it behind a stream)
+    void release_to_caller() { ptr_ = 0; }
     template <typename P>
     P* as() const { return reinterpret_cast<P*>((uintptr_t)ptr_); }
 

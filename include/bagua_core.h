@@ -134,6 +134,13 @@ void bagua_loopback_group_destroy(void* group);
 BaguaSingleCommunicatorC* bagua_loopback_communicator_create(void* group, size_t rank, uint64_t stream_ptr);
 
 /* ------------------------------------------------------------- comm ops -- */
+/* Async mode (off by default): the comm ops below return as soon as their work is
+ * enqueued on the communicator's stream instead of waiting for it (the reference's
+ * datatypes/mod.rs:1062-1066 sync); their temporary buffers go back to the pool
+ * behind the stream.  Synchronise the stream (bagua_comm_synchronize) before
+ * reading a result on the host.  The native scheduler runs its ops this way and
+ * waits for each bucket in bagua_comm_backend_wait_pending_comm_ops. */
+int bagua_comm_set_async(BaguaSingleCommunicatorC* comm, int on);
 /* CentralizedLowPrecisionSynchronous::execute_background_communication on one
  * flat communication tensor (centralized_low_precision_synchronous.rs:16-73). */
 int bagua_centralized_low_precision_synchronous(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,

@@ -175,3 +175,51 @@ def test_bucket_readiness_api(bc, comm):
     bk.reset_comm_ready()
     assert not bk.ready_for_comm()
     assert ctypes.c_int(bc._native.C.bagua_bucket_num_ops(bk.handle)).value == 0
+
+
+def test_async_ops_on_a_communicator(bc, oracle_c):
+    """bagua_comm_set_async: ops return once enqueued (their buffers go back to the
+    pool behind the stream); many buckets queued back to back, one sync at the end,
+    every result equal to the oracle's simulation."""
+    N = bc._native
+    stream = torch.cuda.Stream()
+    uid = bc.BaguaSingleCommunicatorPy.generate_nccl_unique_id_str()
+    comm = bc.BaguaSingleCommunicatorPy(0, 1, 0, stream.cuda_stream, uid)
+    assert N.C.bagua_comm_set_async(comm.handle, 1) == 0
+    rng = np.random.default_rng(11)
+    xs = [(rng.standard_normal(3 * 20000 + 96 * i) * 1e-3).astype(np.float32) for i in range(8)]
+    ts = [torch.from_numpy(x).cuda() for x in xs]
+    torch.cuda.synchronize()
+    for rep in range(2):
+        for t in ts:
+            raw = bc.BaguaTensorPy(t, "g").raw()
+            N.check(N.C.bagua_centralized_low_precision_synchronous(comm.handle, ctypes.byref(raw), 1,
+                                                                    N.COMPRESSION_MINMAX_UINT8), "op")
+    comm.synchronize()
+    for x, t in zip(xs, ts):
+        want = simulate.centralized_low_precision(oracle_c, [x], F32, True)[0]
+        want = simulate.centralized_low_precision(oracle_c, [want], F32, True)[0]
+        assert np.array_equal(t.cpu().numpy().view(np.uint32), want.view(np.uint32))
+    assert N.C.bagua_comm_set_async(comm.handle, 0) == 0
+
+
+def test_backend_sync_mode_env(bc, comm, oracle_c, monkeypatch):
+    """BAGUA_BACKEND_SYNC=1: the worker waits for every op (the reference's behaviour);
+    same results."""
+    monkeypatch.setenv("BAGUA_BACKEND_SYNC", "1")
+    host, parts, _keep = _grads(3, 3 * 30000, 5, True)
+    buckets = []
+    for b in range(3):
+        bk = bc.BaguaBucketPy(f"s{b}", [bc.BaguaTensorPy(t, f"s{b}.{i}") for i, t in enumerate(parts[b])])
+        bk.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+        buckets.append(bk)
+    backend = bc.BaguaCommBackendPy(4, 0)
+    backend.register_ordered_buckets(buckets)
+    for bk in buckets:
+        for t in bk.tensors():
+            backend.mark_communication_ready(t, 0)
+    assert backend.wait_pending_comm_ops() == 3
+    for b in range(3):
+        want = simulate.centralized_low_precision(oracle_c, [host[b]], F32, True)[0]
+        got = torch.cat([t.reshape(-1) for t in parts[b]]).cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
