@@ -83,7 +83,17 @@ hipStream_t ops_stream(const std::vector<bagua_bucket_op_t>& ops) {
     return nullptr;
 }
 
-int run_op(const bagua_bucket_op_t& op, const bagua_tensor_t* flat, const char* bucket_name, hipStream_t s) {
+// the ops return once enqueued: run by the scheduler's worker, or on a communicator
+// set async (bagua_comm_set_async)
+bool ops_async(const std::vector<bagua_bucket_op_t>& ops) {
+    if (g_async_ops) return true;
+    for (const bagua_bucket_op_t& op : ops)
+        if (op.comm && op.comm->async) return true;
+    return false;
+}
+
+int run_op(const bagua_bucket_op_t& op, const bagua_tensor_t* flat, const char* bucket_name, hipStream_t s,
+           bool async) {
     switch (op.kind) {
         case BAGUA_BUCKET_OP_CENTRALIZED_LOW_PRECISION:
             return op.fused ? bagua_centralized_low_precision_synchronous(op.comm, flat, op.average, op.compression)
@@ -97,7 +107,7 @@ int run_op(const bagua_bucket_op_t& op, const bagua_tensor_t* flat, const char* 
         case BAGUA_BUCKET_OP_CALLBACK:
             // the callback sees the previous ops' results, as in the reference (their
             // Drop synced), also when the worker runs the ops async
-            if (g_async_ops && hipStreamSynchronize(s) != hipSuccess) return BAGUA_ERR_HIP;
+            if (async && s && hipStreamSynchronize(s) != hipSuccess) return BAGUA_ERR_HIP;
             if (op.callback) op.callback(op.user, bucket_name);  // python_ffi_op.rs: call with the bucket name
             return BAGUA_OK;
     }
@@ -129,6 +139,7 @@ int execute_bucket(BaguaBucketC* b, const std::vector<uint64_t>& events, const s
     for (uint64_t ev : events)  // :969-980 the stream waits for every tensor's ready event
         if (hipStreamWaitEvent(s, (hipEvent_t)(uintptr_t)ev, 0) != hipSuccess) return BAGUA_ERR_HIP;
     if (ops.empty()) return BAGUA_OK;
+    const bool async = ops_async(ops);
     const size_t esz = bagua_dtype_bytes(first.dtype);
     uint64_t total_alloc = 0, total = 0;
     for (const BucketTensor& t : b->tensors) {
@@ -139,7 +150,7 @@ int execute_bucket(BaguaBucketC* b, const std::vector<uint64_t>& events, const s
     if (contiguous(b)) {
         const bagua_tensor_t flat{first.ptr, total_alloc, total_alloc, first.dtype, first.device_id};
         for (const bagua_bucket_op_t& op : ops)
-            if ((rc = run_op(op, &flat, b->name.c_str(), s)) != BAGUA_OK) break;
+            if ((rc = run_op(op, &flat, b->name.c_str(), s, async)) != BAGUA_OK) break;
         return rc;
     }
     // :999-1038 pack num_elements() of every tensor into a pool buffer on the stream
@@ -155,7 +166,7 @@ int execute_bucket(BaguaBucketC* b, const std::vector<uint64_t>& events, const s
     }
     const bagua_tensor_t flat{buf.ptr(), total, total_alloc, first.dtype, first.device_id};
     for (const bagua_bucket_op_t& op : ops)
-        if ((rc = run_op(op, &flat, b->name.c_str(), s)) != BAGUA_OK) break;
+        if ((rc = run_op(op, &flat, b->name.c_str(), s, async)) != BAGUA_OK) break;
     // :1043-1070 copy back, then wait for the stream (the buffer returns to the pool);
     // async: the buffer returns to the pool behind the stream instead
     const uint8_t* src = buf.as<uint8_t>();
@@ -166,7 +177,7 @@ int execute_bucket(BaguaBucketC* b, const std::vector<uint64_t>& events, const s
             rc = BAGUA_ERR_HIP;
         src += bytes;
     }
-    if (g_async_ops) {
+    if (async) {
         const uint64_t sv = (uint64_t)(uintptr_t)s;
         const uint64_t p = buf.ptr();
         buf.release_to_caller();
@@ -312,7 +323,11 @@ int bagua_bucket_clear_ops(BaguaBucketC* b) {
     return BAGUA_OK;
 }
 
-int bagua_bucket_num_ops(BaguaBucketC* b) { return b ? (int)b->ops.size() : -1; }
+int bagua_bucket_num_ops(BaguaBucketC* b) {
+    if (!b) return -1;
+    std::lock_guard<std::mutex> g(b->mu);
+    return (int)b->ops.size();
+}
 
 int bagua_bucket_mark_tensor_ready(BaguaBucketC* b, const char* tensor_name, uint64_t ready_event) {
     if (!b || !tensor_name) return BAGUA_ERR_INVALID_ARG;

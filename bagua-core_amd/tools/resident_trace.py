@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--cfgs", default="0,1,2,3,4,5")
     ap.add_argument("--runs", type=int, default=10)
     ap.add_argument("--decode", action="store_true", help="run the decode between encodes (bench step)")
+    ap.add_argument("--dump", default="", help="also save the raw stamps (runs x workgroups x 8, us) to this .npy")
     a = ap.parse_args()
     n = a.elements
     dev = torch.device("cuda", 0)
@@ -58,7 +59,9 @@ def main():
                 t = tr.cpu().numpy().reshape(cus, 8).astype(np.float64) * (1e3 / khz)  # us
                 t -= t[:, 0].min()
                 rows.append(t)
-        t = np.stack(rows)  # runs x wg x 4
+        t = np.stack(rows)  # runs x wg x 8
+        if a.dump:
+            np.save(a.dump.replace(".npy", f"_cfg{cfg}.npy"), t)
         out = {
             "cfg": cfg,
             "start_spread_us": float(np.median(t[:, :, 0].max(axis=1))),
