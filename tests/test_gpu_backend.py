@@ -12,6 +12,7 @@ BaguaBucket (datatypes/mod.rs:1072-1267) semantics:
   contiguous buckets (in place) and scattered ones (packed + copied back).
 """
 import ctypes
+import threading
 
 import numpy as np
 import pytest
@@ -223,3 +224,56 @@ def test_backend_sync_mode_env(bc, comm, oracle_c, monkeypatch):
         want = simulate.centralized_low_precision(oracle_c, [host[b]], F32, True)[0]
         got = torch.cat([t.reshape(-1) for t in parts[b]]).cpu().numpy()
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("p", [2, 4])
+def test_scheduler_multirank_loopback(bc, oracle_c, p):
+    """p virtual ranks on the loopback transport, each with its own scheduler (worker
+    thread, async ops) and the same ordered buckets: every rank's workers meet in the
+    collectives, and every bucket on every rank equals the oracle's simulation of the
+    reference op across the ranks (bit-for-bit).  Buckets are marked ready in reverse
+    order, as backward produces them; the scheduler runs them in registration order."""
+    from bagua_core.communicator import loopback_communicators
+    comms = loopback_communicators(p, 0)
+    n_buckets, per = 5, 3 * 4096 * p
+    rng = np.random.default_rng(100 + p)
+    host = [[(rng.standard_normal(per) * 1e-3).astype(np.float32) for _ in range(n_buckets)] for _ in range(p)]
+    flats = [[torch.from_numpy(h.copy()).cuda() for h in host[r]] for r in range(p)]
+    seen = [[] for _ in range(p)]
+    backends, tensors = [], []
+    for r in range(p):
+        buckets, ts_r = [], []
+        for b in range(n_buckets):
+            ts = [bc.BaguaTensorPy(v, f"g{b}.{i}") for i, v in enumerate(flats[r][b].view(3, -1).unbind(0))]
+            bk = bc.BaguaBucketPy(f"bucket{b}", ts)
+            bk.append_centralized_synchronous_op(comms[r], None, False, True, False, "MinMaxUInt8")
+            bk.append_python_op(lambda name, r=r: seen[r].append(name))
+            buckets.append(bk)
+            ts_r.append(ts)
+        be = bc.BaguaCommBackendPy(2, 0)
+        be.register_ordered_buckets(buckets)
+        backends.append((be, buckets))
+        tensors.append(ts_r)
+    torch.cuda.synchronize()
+    for it in range(2):
+        done = [None] * p
+
+        def rank(r):  # one host thread per rank, as one process per GPU would be
+            for b in reversed(range(n_buckets)):
+                for t in tensors[r][b]:
+                    backends[r][0].mark_communication_ready(t, 0)
+            done[r] = backends[r][0].wait_pending_comm_ops()
+        ths = [threading.Thread(target=rank, args=(r,)) for r in range(p)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join(timeout=120)
+        assert done == [n_buckets] * p, done
+        for b in range(n_buckets):
+            want = simulate.centralized_low_precision(oracle_c, [host[r][b] for r in range(p)], F32, True)
+            for r in range(p):
+                host[r][b] = want[r]
+                got = flats[r][b].cpu().numpy()
+                assert np.array_equal(got.view(np.uint32), want[r].view(np.uint32)), (it, b, r)
+    assert all(s == [f"bucket{b}" for b in range(n_buckets)] * 2 for s in seen), seen
+    del backends
