@@ -141,6 +141,9 @@ CORE_SIGNATURES = {
     "bagua_pool_free_after": (_i32, [_u64, ctypes.POINTER(ctypes.c_uint64), _i32]),
     "bagua_pool_trim": (_i32, [_i32]),
     "bagua_pool_bytes_pending": (_sz, [_i32]),
+    "bagua_pool_capture_begin": (_vp, []),
+    "bagua_pool_capture_end": (_i32, [_vp]),
+    "bagua_pool_capture_release": (_i32, [_vp]),
     "bagua_release_stream_resources": (_i32, [_i32, _u64]),
     "bagua_stream_workspace_count": (_sz, []),
     "bagua_pool_bytes_in_use": (_sz, [_i32]),

@@ -83,16 +83,38 @@ void reap_pending(DevicePool& d, bool wait) {
     d.pending.resize(keep);
 }
 
+// Capture arena: while the calling thread captures a HIP graph, every block its
+// ops take from the pool belongs to the graph (the graph's kernels address it on
+// every replay), so frees inside the capture are deferred to the arena's release
+// and no pool call queries events (a query during capture invalidates it).
+struct CaptureArena {
+    std::vector<uint64_t> held;
+};
+thread_local CaptureArena* t_arena = nullptr;
+
+bool arena_holds(uint64_t ptr) {
+    if (!t_arena) return false;
+    for (uint64_t p : t_arena->held)
+        if (p == ptr) return true;
+    return false;
+}
+
 }  // namespace
 
 int pool_alloc(int device_id, size_t bytes, uint64_t* out) {
     if (!out) return BAGUA_ERR_INVALID_ARG;
+    const int rc = pool_alloc_block(device_id, bytes, out);
+    if (rc == BAGUA_OK && t_arena) t_arena->held.push_back(*out);
+    return rc;
+}
+
+int pool_alloc_block(int device_id, size_t bytes, uint64_t* out) {
     const size_t cls = size_class(bytes ? bytes : 1);
     Pool& P = pool();
     {
         std::lock_guard<std::mutex> g(P.mu);
         DevicePool& d = P.dev[device_id];
-        if (!d.pending.empty()) reap_pending(d, false);
+        if (!d.pending.empty() && !t_arena) reap_pending(d, false);
         auto it = d.free_blocks.find(cls);
         if (it != d.free_blocks.end() && !it->second.empty()) {
             *out = it->second.back();
@@ -125,6 +147,11 @@ int pool_alloc(int device_id, size_t bytes, uint64_t* out) {
 
 int pool_free(uint64_t ptr) {
     if (!ptr) return BAGUA_OK;
+    if (arena_holds(ptr)) return BAGUA_OK;  // the graph keeps it (capture_release frees it)
+    return pool_free_block(ptr);
+}
+
+int pool_free_block(uint64_t ptr) {
     Pool& P = pool();
     std::lock_guard<std::mutex> g(P.mu);
     auto it = P.live.find(ptr);
@@ -141,6 +168,7 @@ int pool_free(uint64_t ptr) {
 
 int pool_free_after(uint64_t ptr, const uint64_t* streams, int n) {
     if (!ptr) return BAGUA_OK;
+    if (arena_holds(ptr)) return BAGUA_OK;
     if (n <= 0) return pool_free(ptr);
     if (!streams) return BAGUA_ERR_INVALID_ARG;
     Pool& P = pool();
@@ -201,6 +229,30 @@ int pool_trim(int device_id) {
     return BAGUA_OK;
 }
 
+void* pool_capture_begin() {
+    if (t_arena) return nullptr;  // no nesting
+    t_arena = new CaptureArena();
+    return t_arena;
+}
+
+int pool_capture_end(void* arena) {
+    if (!arena || arena != t_arena) return BAGUA_ERR_INVALID_ARG;
+    t_arena = nullptr;
+    return BAGUA_OK;
+}
+
+int pool_capture_release(void* arena) {
+    if (!arena || arena == t_arena) return BAGUA_ERR_INVALID_ARG;
+    CaptureArena* a = static_cast<CaptureArena*>(arena);
+    int rc = BAGUA_OK;
+    for (uint64_t p : a->held) {
+        const int r = pool_free_block(p);
+        if (r && !rc) rc = r;
+    }
+    delete a;
+    return rc;
+}
+
 size_t pool_bytes_pending(int device_id) {
     Pool& P = pool();
     std::lock_guard<std::mutex> g(P.mu);
@@ -226,6 +278,9 @@ int bagua_pool_free_after(uint64_t ptr, const uint64_t* streams, int n) {
 }
 int bagua_pool_trim(int device_id) { return bagua::pool_trim(device_id); }
 size_t bagua_pool_bytes_pending(int device_id) { return bagua::pool_bytes_pending(device_id); }
+void* bagua_pool_capture_begin(void) { return bagua::pool_capture_begin(); }
+int bagua_pool_capture_end(void* arena) { return bagua::pool_capture_end(arena); }
+int bagua_pool_capture_release(void* arena) { return bagua::pool_capture_release(arena); }
 size_t bagua_pool_bytes_in_use(int device_id) { return bagua::pool_bytes(device_id, false); }
 size_t bagua_pool_bytes_cached(int device_id) { return bagua::pool_bytes(device_id, true); }
 }

@@ -15,6 +15,11 @@ int pool_alloc(int device_id, size_t bytes, uint64_t* out);
 int pool_free(uint64_t ptr);
 int pool_free_after(uint64_t ptr, const uint64_t* streams, int n);
 int pool_trim(int device_id);
+int pool_alloc_block(int device_id, size_t bytes, uint64_t* out);  // no capture-arena bookkeeping
+int pool_free_block(uint64_t ptr);
+void* pool_capture_begin();
+int pool_capture_end(void* arena);
+int pool_capture_release(void* arena);
 size_t pool_bytes(int device_id, bool cached);
 size_t pool_bytes_pending(int device_id);
 

@@ -64,6 +64,13 @@ int bagua_pool_free_after(uint64_t ptr, const uint64_t* streams, int n);
 int bagua_pool_trim(int device_id);
 /* Blocks freed with bagua_pool_free_after whose streams have not drained yet. */
 size_t bagua_pool_bytes_pending(int device_id);
+/* HIP-graph capture of comm ops on the calling thread: between begin and end, the
+ * blocks the ops take from the pool belong to the graph (frees are deferred) and the
+ * pool queries no events.  Release the arena once the graph is destroyed and no
+ * replay is in flight.  Returns NULL when an arena is already open on this thread. */
+void* bagua_pool_capture_begin(void);
+int bagua_pool_capture_end(void* arena);
+int bagua_pool_capture_release(void* arena);
 /* Drops `stream`'s per-stream workspace and its one-launch encode slot after the
  * stream has drained.  Communicator teardown calls it for its streams; call it
  * before destroying any other stream that ran codec calls. */

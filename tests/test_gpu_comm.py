@@ -3,6 +3,8 @@
 gloo in tests/test_distributed_sim.py and by construction), and of the
 bucket / scheduler surface.  Results are compared bit-exact with the oracle
 simulation of the reference op sequence (oracle/simulate.py)."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -137,3 +139,54 @@ def test_pool_reuse(bc):
     assert p2.value == p1.value  # same size class -> block reused
     assert N.C.bagua_pool_free(p2.value) == 0
     assert N.C.bagua_pool_free(12345) != 0
+
+
+@pytest.mark.parametrize("method", ["MinMaxUInt8", "OneBit"])
+def test_op_captured_into_a_hip_graph(bc, comm, oracle_c, method):
+    """The compressed centralized op (async mode) captured into a HIP graph between
+    bagua_pool_capture_begin/end: the graph owns the op's pool blocks, every replay
+    on new data equals the eager op bit-for-bit, and the arena gives the blocks back
+    once the graph is gone."""
+    N = bc._native
+    code = N.COMPRESSION_MINMAX_UINT8 if method == "MinMaxUInt8" else N.COMPRESSION_ONEBIT
+    assert N.C.bagua_comm_set_async(comm.handle, 1) == 0
+    try:
+        n = 3 * 65536
+        rng = np.random.default_rng(77)
+        xs = [(rng.standard_normal(n) * 1e-3).astype(np.float32) for _ in range(3)]
+        t = torch.zeros(n, device="cuda")
+        raw = bc.BaguaTensorPy(t, "g").raw()
+
+        def op():
+            N.check(N.C.bagua_centralized_low_precision_synchronous(comm.handle, ctypes.byref(raw), 1, code), "op")
+
+        want = []
+        for x in xs:  # eager results (and a warm pool)
+            t.copy_(torch.from_numpy(x))
+            op()
+            comm.synchronize()
+            want.append(t.cpu().numpy().copy())
+        stream = comm._keep_stream
+        in_use = N.C.bagua_pool_bytes_in_use(0)
+        g = torch.cuda.CUDAGraph()
+        arena = N.C.bagua_pool_capture_begin()
+        assert arena
+        try:
+            with torch.cuda.graph(g, stream=stream, capture_error_mode="relaxed"):
+                op()
+        finally:
+            assert N.C.bagua_pool_capture_end(arena) == 0
+        held = N.C.bagua_pool_bytes_in_use(0) - in_use
+        assert held > 0  # the compressed buffers stay with the graph
+        for x, w in zip(reversed(xs), reversed(want)):
+            t.copy_(torch.from_numpy(x))
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            assert np.array_equal(t.cpu().numpy().view(np.uint32), w.view(np.uint32))
+        del g
+        torch.cuda.synchronize()
+        assert N.C.bagua_pool_capture_release(arena) == 0
+        assert N.C.bagua_pool_bytes_in_use(0) == in_use
+    finally:
+        assert N.C.bagua_comm_set_async(comm.handle, 0) == 0
