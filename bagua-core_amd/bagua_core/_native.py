@@ -46,7 +46,7 @@ class bagua_bucket_op_t(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("average", ctypes.c_int32), ("compression", ctypes.c_int32),
                 ("fused", ctypes.c_int32), ("comm", ctypes.c_void_p), ("weight", bagua_tensor_t),
                 ("left_peer_weight", bagua_tensor_t), ("right_peer_weight", bagua_tensor_t),
-                ("callback", ctypes.c_void_p), ("user", ctypes.c_void_p)]
+                ("callback", ctypes.c_void_p), ("user", ctypes.c_void_p), ("intranode", ctypes.c_void_p)]
 
 
 BUCKET_OP_CENTRALIZED_LOW_PRECISION, BUCKET_OP_CENTRALIZED_FULL_PRECISION = 1, 2
@@ -167,6 +167,11 @@ CORE_SIGNATURES = {
     "bagua_comm_allreduce_inplace": (_i32, [_C, _T, _i32]),
     "bagua_comm_allreduce": (_i32, [_C, _T, _T, _i32]),
     "bagua_comm_broadcast": (_i32, [_C, _T, _i32]),
+    "bagua_comm_reduce_inplace": (_i32, [_C, _T, _i32, _i32]),
+    "bagua_comm_reduce": (_i32, [_C, _T, _T, _i32, _i32]),
+    "bagua_centralized_low_precision_hierarchical": (_i32, [_C, _C, _T, _i32, _i32]),
+    "bagua_centralized_full_precision_hierarchical": (_i32, [_C, _C, _T, _i32]),
+    "bagua_decentralized_low_precision_hierarchical": (_i32, [_C, _C, _T, _T, _T, _T, _i32]),
     "bagua_comm_alltoall": (_i32, [_C, _T, _T]),
     "bagua_comm_alltoall_inplace": (_i32, [_C, _T]),
     "bagua_comm_allgather_inplace": (_i32, [_C, _T]),

@@ -30,43 +30,50 @@ from .tensor import BaguaTensorPy, compression_code
 CALLBACK = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_char_p)
 
 
+def _handle(c: Optional[BaguaSingleCommunicatorPy]):
+    return c.handle.value if c is not None else None
+
+
 @dataclass
 class CentralizedLowPrecisionSynchronous:
-    communicator: BaguaSingleCommunicatorPy
+    communicator: Optional[BaguaSingleCommunicatorPy]  # internode (None on a hierarchical node worker)
     average: bool
     compression: str
     fused: bool = True
+    intranode: Optional[BaguaSingleCommunicatorPy] = None  # hierarchical mode
 
     def native(self) -> N.bagua_bucket_op_t:
         return N.bagua_bucket_op_t(kind=N.BUCKET_OP_CENTRALIZED_LOW_PRECISION, average=int(self.average),
                                    compression=compression_code(self.compression), fused=int(self.fused),
-                                   comm=self.communicator.handle.value)
+                                   comm=_handle(self.communicator), intranode=_handle(self.intranode))
 
 
 @dataclass
 class CentralizedFullPrecisionSynchronous:
-    communicator: BaguaSingleCommunicatorPy
+    communicator: Optional[BaguaSingleCommunicatorPy]
     average: bool
+    intranode: Optional[BaguaSingleCommunicatorPy] = None
 
     def native(self) -> N.bagua_bucket_op_t:
         return N.bagua_bucket_op_t(kind=N.BUCKET_OP_CENTRALIZED_FULL_PRECISION, average=int(self.average),
-                                   comm=self.communicator.handle.value)
+                                   comm=_handle(self.communicator), intranode=_handle(self.intranode))
 
 
 @dataclass
 class DecentralizedLowPrecisionSynchronous:
-    communicator: BaguaSingleCommunicatorPy
+    communicator: Optional[BaguaSingleCommunicatorPy]
     compression: str
     weight: BaguaTensorPy
     left_peer_weight: BaguaTensorPy
     right_peer_weight: BaguaTensorPy
+    intranode: Optional[BaguaSingleCommunicatorPy] = None
 
     def native(self) -> N.bagua_bucket_op_t:
         return N.bagua_bucket_op_t(kind=N.BUCKET_OP_DECENTRALIZED_LOW_PRECISION,
                                    compression=compression_code(self.compression),
-                                   comm=self.communicator.handle.value, weight=self.weight.raw(),
+                                   comm=_handle(self.communicator), weight=self.weight.raw(),
                                    left_peer_weight=self.left_peer_weight.raw(),
-                                   right_peer_weight=self.right_peer_weight.raw())
+                                   right_peer_weight=self.right_peer_weight.raw(), intranode=_handle(self.intranode))
 
 
 @dataclass
@@ -146,36 +153,46 @@ class BaguaBucketPy:
                                           communicator_intranode: Optional[BaguaSingleCommunicatorPy] = None,
                                           hierarchical: bool = False, average: bool = True,
                                           scattergather: bool = False, compression: Optional[str] = None) -> None:
-        comm = self._single(communicator_internode, communicator_intranode, hierarchical)
+        comm, intra = self._communicators(communicator_internode, communicator_intranode, hierarchical)
         if compression is None:
             if scattergather:
                 raise NotImplementedError("scattergather full-precision op is outside the compressed-gradient path")
-            self._append(CentralizedFullPrecisionSynchronous(comm, average))
+            self._append(CentralizedFullPrecisionSynchronous(comm, average, intranode=intra))
         else:
             compression_code(compression)
-            self._append(CentralizedLowPrecisionSynchronous(comm, average, compression))
+            self._append(CentralizedLowPrecisionSynchronous(comm, average, compression, intranode=intra))
 
     def append_low_precision_decentralized_synchronous_op(
             self, communicator_internode: Optional[BaguaSingleCommunicatorPy],
             communicator_intranode: Optional[BaguaSingleCommunicatorPy], hierarchical: bool = False,
             peer_selection_mode: str = "ring", compression: str = "MinMaxUInt8", weight: BaguaTensorPy = None,
             left_peer_weight: BaguaTensorPy = None, right_peer_weight: BaguaTensorPy = None) -> None:
-        comm = self._single(communicator_internode, communicator_intranode, hierarchical)
+        comm, intra = self._communicators(communicator_internode, communicator_intranode, hierarchical)
         if peer_selection_mode != "ring":
             # datatypes/mod.rs:1170-1174
             raise NotImplementedError("unsupported peer_selection_mode for low precision decentralized algorithm "
                                       "(should be `ring`)")
         compression_code(compression)
         self._append(DecentralizedLowPrecisionSynchronous(comm, compression, weight, left_peer_weight,
-                                                          right_peer_weight))
+                                                          right_peer_weight, intranode=intra))
 
     @staticmethod
-    def _single(internode, intranode, hierarchical):
-        if hierarchical:
-            raise NotImplementedError("hierarchical communicators are outside the compressed-gradient path")
+    def _communicators(internode, intranode, hierarchical):
+        """BaguaCommunicator::new (communicators/mod.rs:348-383): (internode, None), or in
+        hierarchical mode (internode on the node leader, None on its workers, intranode)."""
+        if not hierarchical:
+            if internode is None:
+                raise RuntimeError("inter node communicator must be given in non-hierarchical mode")
+            return internode, None
+        if intranode is None:
+            raise RuntimeError("intra node communicator must be given in hierarchical mode")
+        if intranode.rank() != 0:
+            return None, intranode  # a node worker: reduce + broadcast only
         if internode is None:
-            raise RuntimeError("cannot create communicator: communicator_internode is None")
-        return internode
+            raise RuntimeError("inter node communicator must be given on the node leader in hierarchical mode")
+        if internode.stream_ptr() != intranode.stream_ptr():
+            raise RuntimeError("intra node communicator should use the same stream as the inter node communicator")
+        return internode, intranode
 
     # ---- readiness (datatypes/mod.rs:1256-1266, 793-813), by tensor name --------
     def mark_tensor_ready(self, tensor: BaguaTensorPy, ready_cuda_event_ptr: int = 0) -> None:

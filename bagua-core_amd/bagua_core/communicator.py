@@ -82,6 +82,12 @@ class BaguaSingleCommunicatorPy:
     def broadcast(self, tensor: BaguaTensorPy, root_rank: int) -> None:
         self._call(N.C.bagua_comm_broadcast, "broadcast", tensor, extra=(root_rank,))
 
+    def reduce(self, send_tensor: BaguaTensorPy, recv_tensor: BaguaTensorPy, dst: int, op: int) -> None:
+        self._call(N.C.bagua_comm_reduce, "reduce", send_tensor, recv_tensor, extra=(dst, op))
+
+    def reduce_inplace(self, tensor: BaguaTensorPy, dst: int, op: int) -> None:
+        self._call(N.C.bagua_comm_reduce_inplace, "reduce", tensor, extra=(dst, op))
+
     def send(self, tensor: BaguaTensorPy, peer_rank: int) -> None:
         self._call(N.C.bagua_comm_send, "send", tensor, extra=(peer_rank,))
 

@@ -78,8 +78,10 @@ bool contiguous(const BaguaBucketC* b) {
 }
 
 hipStream_t ops_stream(const std::vector<bagua_bucket_op_t>& ops) {
-    for (const bagua_bucket_op_t& op : ops)
+    for (const bagua_bucket_op_t& op : ops) {
+        if (op.intranode) return op.intranode->stream;  // hierarchical: the node's stream (communicators/mod.rs:385-392)
         if (op.comm) return op.comm->stream;
+    }
     return nullptr;
 }
 
@@ -88,12 +90,27 @@ hipStream_t ops_stream(const std::vector<bagua_bucket_op_t>& ops) {
 bool ops_async(const std::vector<bagua_bucket_op_t>& ops) {
     if (g_async_ops) return true;
     for (const bagua_bucket_op_t& op : ops)
-        if (op.comm && op.comm->async) return true;
+        if ((op.comm && op.comm->async) || (op.intranode && op.intranode->async)) return true;
     return false;
 }
 
 int run_op(const bagua_bucket_op_t& op, const bagua_tensor_t* flat, const char* bucket_name, hipStream_t s,
            bool async) {
+    if (op.intranode) {  // hierarchical mode (communicators/mod.rs:390-427)
+        switch (op.kind) {
+            case BAGUA_BUCKET_OP_CENTRALIZED_LOW_PRECISION:
+                return bagua_centralized_low_precision_hierarchical(op.intranode, op.comm, flat, op.average,
+                                                                    op.compression);
+            case BAGUA_BUCKET_OP_CENTRALIZED_FULL_PRECISION:
+                return bagua_centralized_full_precision_hierarchical(op.intranode, op.comm, flat, op.average);
+            case BAGUA_BUCKET_OP_DECENTRALIZED_LOW_PRECISION:
+                return bagua_decentralized_low_precision_hierarchical(op.intranode, op.comm, flat, &op.weight,
+                                                                      &op.left_peer_weight, &op.right_peer_weight,
+                                                                      op.compression);
+            default:
+                break;
+        }
+    }
     switch (op.kind) {
         case BAGUA_BUCKET_OP_CENTRALIZED_LOW_PRECISION:
             return op.fused ? bagua_centralized_low_precision_synchronous(op.comm, flat, op.average, op.compression)
@@ -308,7 +325,9 @@ void bagua_bucket_destroy(BaguaBucketC* b) { delete b; }
 
 int bagua_bucket_append_op(BaguaBucketC* b, const bagua_bucket_op_t* op) {
     if (!b || !op) return BAGUA_ERR_INVALID_ARG;
-    if (op->kind != BAGUA_BUCKET_OP_CALLBACK && !op->comm) return BAGUA_ERR_INVALID_ARG;
+    // a node worker in hierarchical mode has no internode communicator
+    if (op->kind != BAGUA_BUCKET_OP_CALLBACK && !op->comm && !op->intranode) return BAGUA_ERR_INVALID_ARG;
+    if (op->intranode && op->intranode->rank == 0 && !op->comm) return BAGUA_ERR_INVALID_ARG;
     if (op->kind < BAGUA_BUCKET_OP_CENTRALIZED_LOW_PRECISION || op->kind > BAGUA_BUCKET_OP_CALLBACK)
         return BAGUA_ERR_UNSUPPORTED;
     std::lock_guard<std::mutex> g(b->mu);

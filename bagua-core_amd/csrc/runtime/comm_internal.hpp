@@ -24,6 +24,8 @@ struct Transport {
     // count is in elements of `dtype` (bagua dtype codes)
     virtual int allreduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t s) = 0;
     virtual int broadcast(void* buf, size_t count, int dtype, int root, hipStream_t s) = 0;
+    // the reduction of every rank's `send` lands in `recv` on `root` (recv is unused elsewhere)
+    virtual int reduce(const void* send, void* recv, size_t count, int dtype, int op, int root, hipStream_t s) = 0;
     // block j of `send` (count elements at j*count) goes to rank j; block j of `recv` comes from rank j
     virtual int alltoall(const void* send, void* recv, size_t count, int dtype, hipStream_t s) = 0;
     // rank j's `count` elements land at recv + j*count (in place when send == recv + rank*count)

@@ -737,6 +737,58 @@ int bagua_decentralized_low_precision_synchronous(BaguaSingleCommunicatorC* c, c
     return decentralized(c, t, weight, left, right, method, true, 0);
 }
 
+}  // extern "C"
+
+// communicators/mod.rs:390-427, execute_communication with a hierarchical
+// communicator (:243-336): every rank of the node reduces (AVG or SUM) into the
+// node leader (intranode rank 0, :264-283 / :312-325), the leader runs the op among
+// the leaders on the internode communicator, and the leader broadcasts the result
+// over the node (:286-294 / :327-330).  The leader's two communicators share one
+// stream and device (:250-256, :356-360).
+template <typename F>
+static int hierarchical(BaguaSingleCommunicatorC* intra, BaguaSingleCommunicatorC* inter, const bagua_tensor_t* t,
+                        bool intranode_average, F&& op) {
+    if (!intra || !intra->t || !t) return BAGUA_ERR_INVALID_ARG;
+    if (intra->aborted.load()) return BAGUA_ERR_ABORTED;
+    const bool leader = intra->rank == 0;
+    if (leader && (!inter || inter->stream != intra->stream || inter->device_id != intra->device_id))
+        return BAGUA_ERR_INVALID_ARG;
+    DeviceGuard guard(intra->device_id);
+    int rc = bagua_comm_reduce_inplace(intra, t, 0, intranode_average ? BAGUA_OP_AVG : BAGUA_OP_SUM);
+    if (!rc && leader) rc = op(inter);
+    if (!rc) rc = bagua_comm_broadcast(intra, t, 0);
+    return finish(intra, rc);
+}
+
+extern "C" {
+
+int bagua_centralized_low_precision_hierarchical(BaguaSingleCommunicatorC* intranode,
+                                                 BaguaSingleCommunicatorC* internode, const bagua_tensor_t* t,
+                                                 int average, int method) {
+    // centralized_low_precision_synchronous.rs:25-30: intranode average = the op's average
+    return hierarchical(intranode, internode, t, average != 0, [&](BaguaSingleCommunicatorC* c) {
+        return bagua_centralized_low_precision_synchronous(c, t, average, method);
+    });
+}
+
+int bagua_centralized_full_precision_hierarchical(BaguaSingleCommunicatorC* intranode,
+                                                  BaguaSingleCommunicatorC* internode, const bagua_tensor_t* t,
+                                                  int average) {
+    return hierarchical(intranode, internode, t, average != 0, [&](BaguaSingleCommunicatorC* c) {
+        return bagua_centralized_full_precision_synchronous(c, t, average);
+    });
+}
+
+int bagua_decentralized_low_precision_hierarchical(BaguaSingleCommunicatorC* intranode,
+                                                   BaguaSingleCommunicatorC* internode, const bagua_tensor_t* t,
+                                                   const bagua_tensor_t* weight, const bagua_tensor_t* left,
+                                                   const bagua_tensor_t* right, int method) {
+    // decentralized_low_precision_synchronous.rs:37-41: the node always averages
+    return hierarchical(intranode, internode, t, true, [&](BaguaSingleCommunicatorC* c) {
+        return bagua_decentralized_low_precision_synchronous(c, t, weight, left, right, method);
+    });
+}
+
 int bagua_decentralized_low_precision_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t,
                                                 const bagua_tensor_t* weight, const bagua_tensor_t* left,
                                                 const bagua_tensor_t* right, int method, int pieces) {

@@ -94,6 +94,9 @@ class RcclTransport final : public Transport {
     int broadcast(void* b, size_t n, int d, int root, hipStream_t st) override {
         return nccl_status(ncclBroadcast(b, b, n, nccl_dtype(d), root, comm_, st));
     }
+    int reduce(const void* s, void* r, size_t n, int d, int op, int root, hipStream_t st) override {
+        return nccl_status(ncclReduce(s, r, n, nccl_dtype(d), nccl_op(op), root, comm_, st));
+    }
     int alltoall(const void* s, void* r, size_t n, int d, hipStream_t st) override {
         return nccl_status(ncclAllToAll(s, r, n, nccl_dtype(d), comm_, st));
     }
@@ -220,6 +223,24 @@ int bagua_comm_broadcast(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, i
     COMM_CHECK(c);
     if (!t) return BAGUA_ERR_INVALID_ARG;
     return c->t->broadcast((void*)(uintptr_t)t->ptr, t->num_elem_allocated, t->dtype, root, c->stream);
+}
+
+int bagua_comm_reduce_inplace(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int root, int op) {
+    // communicators/mod.rs reduce_inplace (count = num_elements_allocated)
+    COMM_CHECK(c);
+    if (!t || root < 0 || (size_t)root >= c->nranks) return BAGUA_ERR_INVALID_ARG;
+    void* p = (void*)(uintptr_t)t->ptr;
+    return c->t->reduce(p, p, t->num_elem_allocated, t->dtype, op, root, c->stream);
+}
+
+int bagua_comm_reduce(BaguaSingleCommunicatorC* c, const bagua_tensor_t* s, const bagua_tensor_t* r, int root,
+                      int op) {
+    COMM_CHECK(c);
+    if (!s || !r || s->dtype != r->dtype || s->num_elem_allocated != r->num_elem_allocated || root < 0 ||
+        (size_t)root >= c->nranks)
+        return BAGUA_ERR_INVALID_ARG;
+    return c->t->reduce((const void*)(uintptr_t)s->ptr, (void*)(uintptr_t)r->ptr, s->num_elem_allocated, s->dtype, op,
+                        root, c->stream);
 }
 
 int bagua_comm_alltoall(BaguaSingleCommunicatorC* c, const bagua_tensor_t* s, const bagua_tensor_t* r) {

@@ -103,6 +103,24 @@ class LoopbackTransport final : public Transport {
         if (copy(rcv, acc.as<void>(), b, st)) return BAGUA_ERR_HIP;
         return hipStreamSynchronize(st) == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP;
     }
+    int reduce(const void* s, void* rcv, size_t n, int d, int op, int root, hipStream_t st) override {
+        // SUM / AVG over ranks in rank order on the root; the others only contribute
+        if (op != BAGUA_OP_SUM && op != BAGUA_OP_AVG) return BAGUA_ERR_UNSUPPORTED;
+        const size_t b = n * bagua_dtype_bytes(d);
+        PoolBuffer acc;
+        if (r_ == root && acc.allocate(g_->device, b ? b : 1)) return BAGUA_ERR_OOM;
+        if (!enter(st, s)) return BAGUA_ERR_COMM;
+        if (r_ == root) {
+            if (copy(acc.as<void>(), g_->ptr[0], b, st)) return BAGUA_ERR_HIP;
+            for (int j = 1; j < g_->p; ++j)
+                if (bagua_add_inplace(d, acc.as<void>(), g_->ptr[j], (int)n, st)) return BAGUA_ERR_HIP;
+            if (op == BAGUA_OP_AVG && bagua_divide_inplace(d, acc.as<void>(), (float)g_->p, (int)n, st))
+                return BAGUA_ERR_HIP;
+        }
+        if (hipStreamSynchronize(st) != hipSuccess || !g_->barrier()) return BAGUA_ERR_COMM;  // all reads of s done
+        if (r_ == root && copy(rcv, acc.as<void>(), b, st)) return BAGUA_ERR_HIP;
+        return hipStreamSynchronize(st) == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP;
+    }
     int send(const void* buf, size_t n, int d, int peer, hipStream_t st) override {
         my_sends_.push_back({peer, const_cast<void*>(buf), n * bagua_dtype_bytes(d)});
         return in_group_ ? BAGUA_OK : flush(st);

@@ -121,6 +121,11 @@ int bagua_comm_allreduce_inplace(BaguaSingleCommunicatorC* comm, const bagua_ten
 int bagua_comm_allreduce(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* send, const bagua_tensor_t* recv,
                          int op);
 int bagua_comm_broadcast(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t, int root);
+/* reduce (communicators/mod.rs reduce / reduce_inplace): the SUM / AVG / ... of every
+ * rank's tensor lands on `root` */
+int bagua_comm_reduce_inplace(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t, int root, int op);
+int bagua_comm_reduce(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* send, const bagua_tensor_t* recv, int root,
+                      int op);
 int bagua_comm_alltoall(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* send, const bagua_tensor_t* recv);
 int bagua_comm_alltoall_inplace(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t);
 int bagua_comm_allgather_inplace(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t);
@@ -206,6 +211,20 @@ int bagua_ring_exchange_plan(int nranks, int rank, int chunk_size, int pieces, i
                              size_t* relay_bytes);
 int bagua_ring_exchange_ops(int nranks, int rank, int chunk_size, int pieces, int multipath, int group,
                             bagua_p2p_op_t* ops, int max_ops);
+/* Hierarchical mode (communicators/mod.rs:243-427): intranode reduce (AVG when the op
+ * averages; always AVG for the decentralized op) into intranode rank 0, the op among
+ * the node leaders on `internode` (needed on the leader only, same stream and device as
+ * `intranode`), intranode broadcast from rank 0.  Workers pass internode = NULL. */
+int bagua_centralized_low_precision_hierarchical(BaguaSingleCommunicatorC* intranode,
+                                                 BaguaSingleCommunicatorC* internode, const bagua_tensor_t* t,
+                                                 int average, int method);
+int bagua_centralized_full_precision_hierarchical(BaguaSingleCommunicatorC* intranode,
+                                                  BaguaSingleCommunicatorC* internode, const bagua_tensor_t* t,
+                                                  int average);
+int bagua_decentralized_low_precision_hierarchical(BaguaSingleCommunicatorC* intranode,
+                                                   BaguaSingleCommunicatorC* internode, const bagua_tensor_t* t,
+                                                   const bagua_tensor_t* weight, const bagua_tensor_t* left,
+                                                   const bagua_tensor_t* right, int method);
 /* the reference's unfused op sequence (3 addmul, compress, 3 x decompress + add, clone), for A/B */
 int bagua_decentralized_low_precision_synchronous_unfused(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t,
                                                           const bagua_tensor_t* weight,
@@ -236,6 +255,9 @@ typedef struct bagua_bucket_op {
     bagua_tensor_t weight, left_peer_weight, right_peer_weight; /* decentralized op */
     void (*callback)(void* user, const char* bucket_name);     /* BAGUA_BUCKET_OP_CALLBACK */
     void* user;
+    /* hierarchical mode when set: the node's communicator (comm = the internode one,
+     * NULL on the node's workers), see bagua_*_hierarchical */
+    BaguaSingleCommunicatorC* intranode;
 } bagua_bucket_op_t;
 
 /* NULL on error (*status says why): empty list, mixed dtype / device, allocated < num_elem */

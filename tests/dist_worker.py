@@ -277,3 +277,43 @@ def decentralized_multipath_rank(rank: int, world: int, port: int, inputs_path: 
                  l=l.view(np.uint8), r=r.view(np.uint8))
     finally:
         dist.destroy_process_group()
+
+
+def hierarchical_rank(rank: int, world: int, port: int, inputs_path: str, out_dir: str, per_node: int) -> None:
+    """Hierarchical mode (communicators/mod.rs:243-427, comm_ops.cpp hierarchical):
+    reduce (AVG) into the node leader over the node's group, the compressed op among
+    the leaders over their own group, broadcast from the leader over the node."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        nodes = world // per_node
+        node, local = divmod(rank, per_node)
+        # every process creates every group, in the same order (torch.distributed rule)
+        intra = [dist.new_group(list(range(k * per_node, (k + 1) * per_node))) for k in range(nodes)]
+        inter = dist.new_group([k * per_node for k in range(nodes)])
+        with np.load(inputs_path, allow_pickle=False) as z:
+            t = z[f"x{rank}"].copy()
+        leader = node * per_node
+        buf = torch.from_numpy(t)
+        dist.reduce(buf, dst=leader, op=dist.ReduceOp.SUM, group=intra[node])  # 2 ranks: x0 + x1 either way
+        if local == 0:
+            t = (buf.numpy() / np.float32(per_node)).astype(np.float32)  # AVG
+            p = nodes
+            send = C.compress_minmax_u8(t, 0, p, -1)
+            S = send.size
+            recv = torch.empty(S, dtype=torch.uint8)
+            dist.all_to_all_single(recv, torch.from_numpy(send), group=inter)
+            C.decompress_minmax_u8(recv.numpy(), p, t, 0)
+            C.reduce_chunks(t, 0, p, node, True)
+            C.compress_minmax_u8(t, 0, p, node, out=send)
+            cnt = S // p
+            gathered = torch.empty(S, dtype=torch.uint8)
+            dist.all_gather_into_tensor(gathered, torch.from_numpy(send[node * cnt:(node + 1) * cnt].copy()),
+                                        group=inter)
+            C.decompress_minmax_u8(gathered.numpy(), p, t, 0)
+            buf = torch.from_numpy(t)
+        dist.broadcast(buf, src=leader, group=intra[node])
+        np.save(os.path.join(out_dir, f"out{rank}.npy"), buf.numpy().view(np.uint8))
+    finally:
+        dist.destroy_process_group()

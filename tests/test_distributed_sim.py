@@ -167,3 +167,25 @@ def test_decentralized_multipath_gloo(tmp_path, world, pieces, dtype):
         with np.load(tmp_path / f"dec{r}.npz", allow_pickle=False) as z:
             for k, wk in zip("twlr", want):
                 assert np.array_equal(z[k], wk[r].view(np.uint8)), f"rank {r} {k}"
+
+
+@pytest.mark.parametrize("nodes", [2, 4])
+def test_hierarchical_gloo(tmp_path, nodes):
+    """Hierarchical mode with real process groups: 2 ranks per node, node averages
+    reduced into the leaders, the compressed op among the leaders, broadcast back;
+    every rank equals the simulation of the leaders' op on the node averages."""
+    oracle_c.build()
+    per_node, cs = 2, 4096
+    world = nodes * per_node
+    rng = np.random.default_rng(40 + nodes)
+    xs = [(rng.standard_normal(nodes * cs) * 1e-3).astype(np.float32) for _ in range(world)]
+    inputs = tmp_path / "in.npz"
+    np.savez(inputs, **{f"x{r}": x for r, x in enumerate(xs)})
+    mp.spawn(dist_worker.hierarchical_rank, args=(world, _free_port(), str(inputs), str(tmp_path), per_node),
+             nprocs=world, join=True)
+    node_avg = [((xs[k * per_node] + xs[k * per_node + 1]).astype(np.float32) / np.float32(per_node)).astype(np.float32)
+                for k in range(nodes)]
+    want = simulate.centralized_low_precision(oracle_c, node_avg, 0, True)
+    for r in range(world):
+        out = np.load(tmp_path / f"out{r}.npy")
+        assert np.array_equal(out, want[r // per_node].view(np.uint8)), f"rank {r}"
