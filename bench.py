@@ -42,6 +42,14 @@ if int(os.environ.get("WORLD_SIZE", "1")) > 1:
     # one queue serialise (profiles/r02_host_copy_ab.jsonl shows what that costs).
     # 8 keeps the op's streams on queues of their own.  Set before HIP initialises.
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    if os.environ.get("BAGUA_BENCH_SHARED_GPU"):
+        # rehearsal of the N > 1 line on a one-GPU box (tests/test_gpu_rccl_procs.py): every
+        # rank on device 0, each its own "host" to RCCL (which refuses two ranks of one
+        # communicator on one GPU of one host), so RCCL links them by its socket transport.
+        # Exercises the code path, not the xGMI speed.
+        os.environ["NCCL_HOSTID"] = f"bagua-bench-rank-{os.environ.get('RANK', '0')}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ["LOCAL_RANK"] = "0"
 
 import torch  # noqa: E402
 
@@ -545,7 +553,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         # config 5: bf16 bucket, decentralized ring exchange with the uint8 codec
         # (decentralized_low_precision_synchronous.rs:42-152), 2^27 elements per rank
         try:
-            nb = 1 << 27
+            nb = args.elements or (1 << 27)  # config 5: 2^27 bf16 (256 MiB) per rank
             bufs = [(torch.randn(nb, device=dev, generator=g) * 1e-3).to(torch.bfloat16) for _ in range(4)]
             draws = [BaguaTensorPy(b, k).raw() for b, k in zip(bufs, "twlr")]
 

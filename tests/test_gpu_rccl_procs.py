@@ -1,0 +1,171 @@
+"""Multi-process RCCL tests on the box's one MI355X (tests/rccl_worker.py).
+
+Every rank is its own process with its own RCCL communicator; the ranks share
+the GPU and RCCL carries their bytes over its socket transport (each worker
+sets a distinct NCCL_HOSTID, see rccl_worker.py).  This runs the comm ops —
+the pipelined centralized op (MinMax and 1-bit), the pipelined ring op incl.
+the multipath exchange from 6 ranks, hierarchical mode, the native scheduler —
+through real RCCL grouped send/recv, alltoall and allgather across processes,
+which the in-process loopback transport (test_gpu_multirank.py) only emulates
+and the gloo rehearsals (test_distributed_sim.py) run without RCCL.  Every
+rank's bytes must equal the oracle simulation of the reference op sequence.
+Nothing here measures speed: the socket transport is not the xGMI path.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import oracle_np as NP
+from oracle import simulate
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "rccl_worker.py")
+F32, F16, BF16 = 0, 1, 2
+TIMEOUT_S = 90
+
+
+def run_procs(tmp_path, scenario: str, world: int, inputs: dict, **kw) -> list[dict]:
+    np.savez(tmp_path / "inputs.npz", **inputs)
+    procs = []
+    for r in range(world):
+        env = dict(os.environ)
+        env.update({"NCCL_HOSTID": f"bagua-test-rank-{r}", "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1",
+                    "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+        log = open(tmp_path / f"rank{r}.log", "w")
+        procs.append((subprocess.Popen([sys.executable, "-u", WORKER, scenario, str(r), str(world), str(tmp_path)] +
+                                       [f"{k}={v}" for k, v in kw.items()],
+                                       stdout=log, stderr=subprocess.STDOUT, env=env, cwd=ROOT), log))
+    failed = []
+    for r, (p, log) in enumerate(procs):
+        try:
+            rc = p.wait(timeout=TIMEOUT_S)
+        except subprocess.TimeoutExpired:
+            for q, _ in procs:
+                q.kill()
+            rc = "timeout"
+        log.close()
+        if rc != 0:
+            failed.append(r)
+    if failed:
+        tails = "\n".join(f"--- rank {r}:\n" + (tmp_path / f"rank{r}.log").read_text()[-1500:] for r in failed)
+        pytest.fail(f"{scenario} ranks {failed} failed:\n{tails}")
+    outs = []
+    for r in range(world):
+        with np.load(tmp_path / f"out{r}.npz", allow_pickle=False) as z:
+            outs.append({k: z[k] for k in z.files})
+    return outs
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_collectives(tmp_path, world):
+    rng = np.random.default_rng(world)
+    n = 6 * 1000 + 6
+    xs = [rng.integers(-100, 100, n).astype(np.float32) for _ in range(world)]  # exact sums in any order
+    outs = run_procs(tmp_path, "collectives", world, {f"x{r}": x for r, x in enumerate(xs)})
+    m = n // world * world
+    cnt = m // world
+    total = sum(xs)
+    for r, o in enumerate(outs):
+        assert np.array_equal(o["allreduce"].view(np.float32), total), r
+        want_g = np.concatenate([xs[j][j * cnt:(j + 1) * cnt] for j in range(world)])
+        assert np.array_equal(o["allgather"].view(np.float32), want_g), r
+        want_t = np.concatenate([xs[j][r * cnt:(r + 1) * cnt] for j in range(world)])
+        assert np.array_equal(o["alltoall"].view(np.float32), want_t), r
+        assert np.array_equal(o["broadcast"].view(np.float32), xs[world - 1]), r
+    assert np.array_equal(outs[0]["reduce"].view(np.float32), total)
+
+
+@pytest.mark.parametrize("world,method,dtype,cs,pieces", [
+    (2, "MinMaxUInt8", F32, 3 * 65536, 3),     # pipelined, 3 pieces per chunk
+    (4, "MinMaxUInt8", F32, 40960, 0),         # automatic pieces
+    (3, "MinMaxUInt8", BF16, 3 * 8192, 4),
+    (2, "MinMaxUInt8", F32, 12288, -1),        # the reference's unfused sequence
+    (2, "OneBit", F32, 5 * 4096, 3),
+    (4, "OneBit", BF16, 2 * 4096 + 7, 2),      # ragged last tile
+])
+def test_centralized_ops(tmp_path, oracle_c, world, method, dtype, cs, pieces):
+    rng = np.random.default_rng(world * 31 + cs)
+    xs = [NP.from_f32((rng.standard_normal(world * cs) * 1e-3 + 2e-4 * r).astype(np.float32), dtype)
+          for r in range(world)]
+    if method == "MinMaxUInt8" and oracle_c.minmax_compressed_size(world, cs, dtype) % world:
+        pytest.skip("reference alltoall requires S % nranks == 0")
+    want = simulate.centralized_low_precision(oracle_c, xs, dtype, True,
+                                              method="MinMaxUInt8" if method == "MinMaxUInt8" else "OneBitSignScale")
+    outs = run_procs(tmp_path, "centralized", world, {f"x{r}": x for r, x in enumerate(xs)},
+                     method=method, dtype=dtype, pieces=pieces, repeat=2)
+    for r, o in enumerate(outs):
+        for rep in ("t0", "t1"):  # the op twice on one communicator: same bytes
+            assert np.array_equal(o[rep], want[r].view(np.uint8)), (r, rep)
+
+
+@pytest.mark.parametrize("world,dtype,n,pieces,multipath", [
+    (2, F32, 100003, 3, 0),
+    (3, BF16, 65536 * 2, 0, 0),
+    (6, F32, 6 * 4096 + 100, 2, 1),            # multipath exchange: 3 direct slices + relays
+    (6, BF16, 50000, 1, 1),
+])
+def test_decentralized_ring_op(tmp_path, oracle_c, world, dtype, n, pieces, multipath):
+    rng = np.random.default_rng(world * 7 + n)
+    arrs = {k: [NP.from_f32((rng.standard_normal(n) * 1e-3).astype(np.float32), dtype) for _ in range(world)]
+            for k in "twlr"}
+    want = simulate.decentralized_low_precision(oracle_c, arrs["t"], arrs["w"], arrs["l"], arrs["r"], dtype)
+    inputs = {f"{k}{r}": arrs[k][r] for k in "twlr" for r in range(world)}
+    outs = run_procs(tmp_path, "decentralized", world, inputs, dtype=dtype, pieces=pieces, multipath=multipath)
+    for r, o in enumerate(outs):
+        for i, k in enumerate("twlr"):
+            assert np.array_equal(o[k], want[i][r].view(np.uint8)), (r, k)
+
+
+def test_hierarchical(tmp_path, oracle_c):
+    """2 emulated nodes x 2 ranks: ncclReduce(AVG) into each leader, the compressed op
+    between the leaders, ncclBroadcast back (comm_ops.cpp hierarchical)."""
+    nodes, per_node = 2, 2
+    world = nodes * per_node
+    n = 4 * 8192
+    rng = np.random.default_rng(5)
+    xs = [(rng.standard_normal(n) * 1e-3).astype(np.float32) for _ in range(world)]
+    outs = run_procs(tmp_path, "hierarchical", world, {f"x{r}": x for r, x in enumerate(xs)}, per_node=per_node)
+    # two ranks per node: RCCL's AVG (pre-multiplied or post-divided) is exactly (x0 + x1) / 2
+    avgs = [((xs[2 * k] + xs[2 * k + 1]) / np.float32(2)).astype(np.float32) for k in range(nodes)]
+    want = simulate.centralized_low_precision(oracle_c, avgs, F32, True)
+    for r, o in enumerate(outs):
+        assert np.array_equal(o["t"], want[r // per_node].view(np.uint8)), r
+
+
+def test_bench_line_two_ranks(tmp_path):
+    """bench.py's N > 1 line (config 4 + side lines) end to end under torch.distributed.run
+    with two ranks on the one GPU (BAGUA_BENCH_SHARED_GPU): the pipelined headline must
+    not fall back, and the side measurements must not fail."""
+    import json
+    env = dict(os.environ)
+    env.update({"BAGUA_BENCH_SHARED_GPU": "1", "NCCL_IB_DISABLE": "1", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29517", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "3", "--warmup", "1", "--elements", str(1 << 22)]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["config_index"] == 4
+    assert "headline_fallback" not in d and "side_errors" not in d, d
+    assert d["onebit_allreduce"]["ms_per_step"] > 0 and d["decentralized_bf16"]["ms_per_step"] > 0
+    assert d["roofline"]["frac"] > 0
+
+
+def test_native_scheduler(tmp_path, oracle_c):
+    world, nb, per = 2, 3, 2 * 16384
+    rng = np.random.default_rng(9)
+    xs = {(b, r): (rng.standard_normal(per) * 1e-3).astype(np.float32) for b in range(nb) for r in range(world)}
+    outs = run_procs(tmp_path, "backend", world, {f"b{b}_{r}": x for (b, r), x in xs.items()}, buckets=nb)
+    for b in range(nb):
+        want = simulate.centralized_low_precision(oracle_c, [xs[(b, r)] for r in range(world)], F32, True)
+        for r in range(world):
+            assert np.array_equal(outs[r][f"b{b}"], want[r].view(np.uint8)), (b, r)
