@@ -108,6 +108,7 @@ def main() -> None:
             comm.synchronize()
             out[f"t{_}"] = _host(t)
             t.copy_(_dev(inputs[f"x{rank}"], dtype))
+            torch.cuda.synchronize()  # the reset (current stream) lands before the next op (comm stream)
         comm.barrier()
     elif scenario == "decentralized":
         comm = comm_of("all", rank, world, rank == 0)

@@ -89,6 +89,8 @@ def test_collectives(tmp_path, world):
     (2, "MinMaxUInt8", F32, 12288, -1),        # the reference's unfused sequence
     (2, "OneBit", F32, 5 * 4096, 3),
     (4, "OneBit", BF16, 2 * 4096 + 7, 2),      # ragged last tile
+    (8, "MinMaxUInt8", F32, 8 * 4096, 0),      # the driver's N = 8 shape (smaller bucket)
+    (8, "OneBit", F32, 8 * 4096, 0),
 ])
 def test_centralized_ops(tmp_path, oracle_c, world, method, dtype, cs, pieces):
     rng = np.random.default_rng(world * 31 + cs)
@@ -110,6 +112,7 @@ def test_centralized_ops(tmp_path, oracle_c, world, method, dtype, cs, pieces):
     (3, BF16, 65536 * 2, 0, 0),
     (6, F32, 6 * 4096 + 100, 2, 1),            # multipath exchange: 3 direct slices + relays
     (6, BF16, 50000, 1, 1),
+    (8, BF16, 8 * 8192, 0, 1),                 # config 5's rank count, multipath
 ])
 def test_decentralized_ring_op(tmp_path, oracle_c, world, dtype, n, pieces, multipath):
     rng = np.random.default_rng(world * 7 + n)
@@ -139,22 +142,24 @@ def test_hierarchical(tmp_path, oracle_c):
         assert np.array_equal(o["t"], want[r // per_node].view(np.uint8)), r
 
 
-def test_bench_line_two_ranks(tmp_path):
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_line_multirank(tmp_path, world):
     """bench.py's N > 1 line (config 4 + side lines) end to end under torch.distributed.run
-    with two ranks on the one GPU (BAGUA_BENCH_SHARED_GPU): the pipelined headline must
-    not fall back, and the side measurements must not fail."""
+    with `world` ranks on the one GPU (BAGUA_BENCH_SHARED_GPU): the pipelined headline must
+    not fall back, and the side measurements must not fail (8 ranks: the multipath ring
+    exchange and its direct-exchange side line)."""
     import json
     env = dict(os.environ)
     env.update({"BAGUA_BENCH_SHARED_GPU": "1", "NCCL_IB_DISABLE": "1", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", "--master-port=29517", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={29517 + world}", os.path.join(ROOT, "bench.py"), "--gpus", str(world),
            "--steps", "3", "--warmup", "1", "--elements", str(1 << 22)]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["config_index"] == 4
+    assert d["n_gpus"] == world and d["value"] > 0 and d["config"]["config_index"] == 4
     assert "headline_fallback" not in d and "side_errors" not in d, d
     assert d["onebit_allreduce"]["ms_per_step"] > 0 and d["decentralized_bf16"]["ms_per_step"] > 0
     assert d["roofline"]["frac"] > 0
