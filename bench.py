@@ -525,6 +525,12 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         args.pieces = 1
         t_c = timed(lambda: compressed_step(1), args.steps, args.warmup)
     t_u = side("unpieced", lambda: compressed_step(1))
+    # piece counts either side of the automatic choice (4 per chunk at 1 GiB), so the node's own
+    # run says which count hides the codec best behind its links
+    sweep = {}
+    if world > 1 and not headline_fallback:
+        for q in (2, 8):
+            sweep[str(q)] = side(f"pieces_{q}", lambda q=q: compressed_step(q))
     t_f = side("fp32_allreduce", fp32_step)
     # the same all-reduce with the 1-bit sign+scale codec (this repo's extension:
     # N/8 wire bytes per phase instead of N), fused middle step
@@ -630,6 +636,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     extra = {"per_rank_gib_s": round(per_rank, 2), "fp32_allreduce_gib_s": round(fp32, 2),
              "ratio_vs_fp32": round(per_rank / fp32, 3), "fp32_ms_per_step": round(t_f * 1e3, 3),
              "pieces": args.pieces or "auto", "unpieced_ms_per_step": round(t_u * 1e3, 3),
+             "pieces_sweep_ms_per_step": {q: round(v * 1e3, 3) for q, v in sweep.items()} or None,
              "comm_only_ms": round(t_comm * 1e3, 3),
              "comm_only_note": "RCCL alltoall + in-place allgather of the op's S compressed bytes, nothing else",
              "decentralized_bf16": decentralized,

@@ -162,6 +162,7 @@ def test_bench_line_multirank(tmp_path, world):
     assert d["n_gpus"] == world and d["value"] > 0 and d["config"]["config_index"] == 4
     assert "headline_fallback" not in d and "side_errors" not in d, d
     assert d["onebit_allreduce"]["ms_per_step"] > 0 and d["decentralized_bf16"]["ms_per_step"] > 0
+    assert all(v > 0 for v in d["pieces_sweep_ms_per_step"].values()), d["pieces_sweep_ms_per_step"]
     assert d["roofline"]["frac"] > 0
 
 
