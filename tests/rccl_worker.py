@@ -96,14 +96,15 @@ def main() -> None:
         comm = comm_of("all", rank, world, rank == 0)
         method = {"MinMaxUInt8": N.COMPRESSION_MINMAX_UINT8, "OneBit": N.COMPRESSION_ONEBIT}[kw["method"]]
         pieces = int(kw.get("pieces", 0))
+        average = int(kw.get("average", 1))
         t = _dev(inputs[f"x{rank}"], dtype)
         raw = bc.BaguaTensorPy(t, "g").raw()
         for _ in range(int(kw.get("repeat", 1))):  # the op twice in a row on one communicator
             if pieces < 0:
                 fn = N.C.bagua_centralized_low_precision_synchronous_unfused
-                N.check(fn(comm.handle, ctypes.byref(raw), 1, method), "unfused op")
+                N.check(fn(comm.handle, ctypes.byref(raw), average, method), "unfused op")
             else:
-                N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1, method,
+                N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), average, method,
                                                                       pieces), "pipelined op")
             comm.synchronize()
             out[f"t{_}"] = _host(t)

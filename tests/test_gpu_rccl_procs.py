@@ -82,26 +82,28 @@ def test_collectives(tmp_path, world):
     assert np.array_equal(outs[0]["reduce"].view(np.float32), total)
 
 
-@pytest.mark.parametrize("world,method,dtype,cs,pieces", [
-    (2, "MinMaxUInt8", F32, 3 * 65536, 3),     # pipelined, 3 pieces per chunk
-    (4, "MinMaxUInt8", F32, 40960, 0),         # automatic pieces
-    (3, "MinMaxUInt8", BF16, 3 * 8192, 4),
-    (2, "MinMaxUInt8", F32, 12288, -1),        # the reference's unfused sequence
-    (2, "OneBit", F32, 5 * 4096, 3),
-    (4, "OneBit", BF16, 2 * 4096 + 7, 2),      # ragged last tile
-    (8, "MinMaxUInt8", F32, 8 * 4096, 0),      # the driver's N = 8 shape (smaller bucket)
-    (8, "OneBit", F32, 8 * 4096, 0),
+@pytest.mark.parametrize("world,method,dtype,cs,pieces,average", [
+    (2, "MinMaxUInt8", F32, 3 * 65536, 3, 1),  # pipelined, 3 pieces per chunk
+    (4, "MinMaxUInt8", F16, 4 * 4096, 2, 0),   # reduce_sum (average = False)
+    (3, "OneBit", F32, 3 * 4096, 2, 0),
+    (4, "MinMaxUInt8", F32, 40960, 0, 1),      # automatic pieces
+    (3, "MinMaxUInt8", BF16, 3 * 8192, 4, 1),
+    (2, "MinMaxUInt8", F32, 12288, -1, 1),     # the reference's unfused sequence
+    (2, "OneBit", F32, 5 * 4096, 3, 1),
+    (4, "OneBit", BF16, 2 * 4096 + 7, 2, 1),   # ragged last tile
+    (8, "MinMaxUInt8", F32, 8 * 4096, 0, 1),   # the driver's N = 8 shape (smaller bucket)
+    (8, "OneBit", F32, 8 * 4096, 0, 1),
 ])
-def test_centralized_ops(tmp_path, oracle_c, world, method, dtype, cs, pieces):
+def test_centralized_ops(tmp_path, oracle_c, world, method, dtype, cs, pieces, average):
     rng = np.random.default_rng(world * 31 + cs)
     xs = [NP.from_f32((rng.standard_normal(world * cs) * 1e-3 + 2e-4 * r).astype(np.float32), dtype)
           for r in range(world)]
     if method == "MinMaxUInt8" and oracle_c.minmax_compressed_size(world, cs, dtype) % world:
         pytest.skip("reference alltoall requires S % nranks == 0")
-    want = simulate.centralized_low_precision(oracle_c, xs, dtype, True,
+    want = simulate.centralized_low_precision(oracle_c, xs, dtype, bool(average),
                                               method="MinMaxUInt8" if method == "MinMaxUInt8" else "OneBitSignScale")
     outs = run_procs(tmp_path, "centralized", world, {f"x{r}": x for r, x in enumerate(xs)},
-                     method=method, dtype=dtype, pieces=pieces, repeat=2)
+                     method=method, dtype=dtype, pieces=pieces, repeat=2, average=average)
     for r, o in enumerate(outs):
         for rep in ("t0", "t1"):  # the op twice on one communicator: same bytes
             assert np.array_equal(o[rep], want[r].view(np.uint8)), (r, rep)
