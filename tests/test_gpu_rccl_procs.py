@@ -144,17 +144,21 @@ def test_hierarchical(tmp_path, oracle_c):
         assert np.array_equal(o["t"], want[r // per_node].view(np.uint8)), r
 
 
-@pytest.mark.parametrize("world", [2, 8])
-def test_bench_line_multirank(tmp_path, world):
+@pytest.mark.parametrize("world,fail_headline", [(2, False), (8, False), (2, True)])
+def test_bench_line_multirank(tmp_path, world, fail_headline):
     """bench.py's N > 1 line (config 4 + side lines) end to end under torch.distributed.run
     with `world` ranks on the one GPU (BAGUA_BENCH_SHARED_GPU): the pipelined headline must
     not fall back, and the side measurements must not fail (8 ranks: the multipath ring
-    exchange and its direct-exchange side line)."""
+    exchange and its direct-exchange side line).  fail_headline: the headline's communicator
+    is aborted (BAGUA_BENCH_FAIL_HEADLINE, ncclCommAbort on every rank), so the line must come
+    from the unpieced op on a fresh RCCL communicator, with every side line still measured."""
     import json
     env = dict(os.environ)
     env.update({"BAGUA_BENCH_SHARED_GPU": "1", "NCCL_IB_DISABLE": "1", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    if fail_headline:
+        env["BAGUA_BENCH_FAIL_HEADLINE"] = "1"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr=127.0.0.1", f"--master-port={29517 + world}", os.path.join(ROOT, "bench.py"), "--gpus", str(world),
+           "--master-addr=127.0.0.1", f"--master-port={29517 + world + 20 * fail_headline}", os.path.join(ROOT, "bench.py"), "--gpus", str(world),
            "--steps", "3", "--warmup", "1", "--elements", str(1 << 22)]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -162,9 +166,13 @@ def test_bench_line_multirank(tmp_path, world):
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == world and d["value"] > 0 and d["config"]["config_index"] == 4
-    assert "headline_fallback" not in d and "side_errors" not in d, d
+    assert "side_errors" not in d, d
     assert d["onebit_allreduce"]["ms_per_step"] > 0 and d["decentralized_bf16"]["ms_per_step"] > 0
-    assert all(v > 0 for v in d["pieces_sweep_ms_per_step"].values()), d["pieces_sweep_ms_per_step"]
+    if fail_headline:
+        assert d["headline_fallback"]["headline"].startswith("unpieced") and d["pieces"] == 1, d
+    else:
+        assert "headline_fallback" not in d, d
+        assert all(v > 0 for v in d["pieces_sweep_ms_per_step"].values()), d["pieces_sweep_ms_per_step"]
     assert d["roofline"]["frac"] > 0
 
 
