@@ -387,6 +387,175 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_kernel(
 }
 
 // ------------------------------------------------------------------------
+// The same fused middle step, table-driven.  A reduced element depends only on
+// its p sign bits (segment c decodes to +-scale_c), so every value the
+// reference tree can produce is tabulated once per workgroup in LDS:
+//   p <= 8 : lut[bits] = as_stored(avg ? tree(bits) / p : tree(bits)), 2^p entries;
+//   p <= 16: the tree (BY = 8) is ((s0+s4)+(s2+s6)) + ((s1+s5)+(s3+s7)) with
+//            s_y = (0 + v_y) + v_{y+8}: the even-y half depends on the 8 even
+//            segments' bits, the odd-y half on the 8 odd ones, so two 256-entry
+//            tables and one add (then the average and the rounding to T).
+// The per-element bit indexes come from an 8x8 bit-matrix transpose of the
+// lane's 16-bit fields (row = segment, column = element).  Same expressions,
+// same order, so the same bits as onebit_reduce_encode_kernel.
+// ------------------------------------------------------------------------
+// bit (row r, column c) at position 8r + c  ->  position 8c + r
+__device__ __forceinline__ uint64_t transpose8x8(uint64_t x) {
+    uint64_t t;
+    t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+    x = x ^ t ^ (t << 7);
+    t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+    x = x ^ t ^ (t << 14);
+    t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+    x = x ^ t ^ (t << 28);
+    return x;
+}
+
+// idx[b] (b < 16) = sum over rows k < 8 of bit b of rows[k], << k
+__device__ __forceinline__ void bit_columns(const uint32_t (&rows)[8], uint32_t (&idx)[16]) {
+    uint64_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        lo |= (uint64_t)(rows[k] & 0xffu) << (8 * k);
+        hi |= (uint64_t)((rows[k] >> 8) & 0xffu) << (8 * k);
+    }
+    lo = transpose8x8(lo);
+    hi = transpose8x8(hi);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        idx[b] = (uint32_t)(lo >> (8 * b)) & 0xffu;
+        idx[b + 8] = (uint32_t)(hi >> (8 * b)) & 0xffu;
+    }
+}
+
+// the reference tree over p <= 8 segments for the sign pattern `bits`
+template <int BY>
+__device__ __forceinline__ float lut_tree(int bits, int p, const float* pos, const float* neg) {
+    float s[BY];
+#pragma unroll
+    for (int y = 0; y < BY; ++y) s[y] = 0.0f;
+    for (int r = 0; r * BY < p; ++r)
+#pragma unroll
+        for (int y = 0; y < BY; ++y) {
+            const int c = r * BY + y;
+            if (c < p) s[y] = s[y] + (((bits >> c) & 1) ? neg[c] : pos[c]);
+        }
+    tree_finish<BY>(s);
+    return s[0];
+}
+
+// one half (parity 0: y even, 1: y odd) of the BY = 8 tree; bit k of `bits` is
+// segment 2k + parity
+__device__ __forceinline__ float lut_half(int bits, int parity, int p, const float* pos, const float* neg) {
+    float s[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int y = parity + 2 * m;
+        s[m] = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int c = y + 8 * r;
+            const int k = (c - parity) / 2;
+            if (c < p) s[m] = s[m] + (((bits >> k) & 1) ? neg[c] : pos[c]);
+        }
+    }
+    // h = 4: s_y += s_{y+4}; h = 2: s_y += s_{y+2}  ->  (s[0] + s[2]) + (s[1] + s[3])
+    return (s[0] + s[2]) + (s[1] + s[3]);
+}
+
+// PMAX = 2: p <= 2, the index is read bit by bit; 8: the 8x8 transpose; 16: two tables
+template <typename T, int PMAX, bool STORE>
+__global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
+    const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int p, int average,
+    typename T::storage* __restrict__ chunk, uint8_t* __restrict__ out_seg, float* __restrict__ part) {
+    constexpr bool WIDE = PMAX > 8;
+    __shared__ float pos[kMaxFusedChunks], neg[kMaxFusedChunks];
+    __shared__ float lut[WIDE ? 2 : 1][256];
+    if (threadIdx.x < p) {  // segment c decodes to +-scale_c as stored in T
+        float sc;
+        __builtin_memcpy(&sc, in + (int64_t)threadIdx.x * chunk_offset, 4);
+        pos[threadIdx.x] = as_stored<T>(sc);
+        neg[threadIdx.x] = as_stored<T>(-sc);
+    }
+    __syncthreads();
+    const float pf = (float)p;
+    for (int i = threadIdx.x; i < 256; i += kBlock) {
+        if constexpr (WIDE) {
+            lut[0][i] = lut_half(i, 0, p, pos, neg);
+            lut[1][i] = lut_half(i, 1, p, pos, neg);
+        } else if (i < (1 << p)) {
+            const float v = p <= 4 ? lut_tree<2>(i, p, pos, neg) : lut_tree<4>(i, p, pos, neg);
+            lut[0][i] = as_stored<T>(average ? v / pf : v);
+        }
+    }
+    __syncthreads();
+    using S = typename T::storage;
+    const int lane = lane_id();
+    const int64_t tiles = (cs + kObTile - 1) / kObTile;
+    const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    const bool vec = ((uintptr_t)chunk % (4 * sizeof(S))) == 0;
+    uint8_t* bits = out_seg + 32;
+    for (int64_t t = wave; t < tiles; t += nwaves) {
+        // every segment's 16-bit field of this lane, loaded unconditionally (segments
+        // >= p read the last one and are masked to 0 after the loads)
+        uint32_t f[PMAX];
+#pragma unroll
+        for (int c = 0; c < PMAX; ++c) {
+            const int cc = c < p ? c : p - 1;
+            f[c] = reinterpret_cast<const uint16_t*>(in + (int64_t)cc * chunk_offset + 32 + t * kObTileBytes)[lane];
+        }
+#pragma unroll
+        for (int c = 0; c < PMAX; ++c) f[c] = c < p ? f[c] : 0u;
+        float x[4][4];
+        if constexpr (WIDE) {
+            uint32_t re[8], ro[8], ia[16], ib[16];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { re[k] = f[2 * k]; ro[k] = f[2 * k + 1]; }
+            bit_columns(re, ia);
+            bit_columns(ro, ib);
+#pragma unroll
+            for (int b = 0; b < 16; ++b) {
+                const float v = lut[0][ia[b]] + lut[1][ib[b]];
+                x[b / 4][b % 4] = as_stored<T>(average ? v / pf : v);
+            }
+        } else if constexpr (PMAX == 2) {
+#pragma unroll
+            for (int b = 0; b < 16; ++b) x[b / 4][b % 4] = lut[0][((f[0] >> b) & 1u) | (((f[1] >> b) & 1u) << 1)];
+        } else {
+            uint32_t rows[8], ix[16];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) rows[k] = f[k];
+            bit_columns(rows, ix);
+#pragma unroll
+            for (int b = 0; b < 16; ++b) x[b / 4][b % 4] = lut[0][ix[b]];
+        }
+        uint32_t field = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t j = t * kObTile + k * 256 + lane * 4 + e;
+                if (j >= cs) x[k][e] = 0.0f;  // padding past cs stays 0 (as the encoder sees it)
+                field |= (x[k][e] < 0.0f ? 1u : 0u) << (k * 4 + e);
+            }
+        if constexpr (STORE) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) store4<T>(chunk, t * kObTile + k * 256 + lane * 4, cs, vec, x[k]);
+        }
+        const uint32_t next = (uint32_t)__shfl_down((int)field, 1, kWave);
+        if ((lane & 1) == 0) reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane >> 1] = field | (next << 16);
+        float ab[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ab[k][e] = __builtin_fabsf(x[k][e]);
+        const float sum = wave_tree_sum(lane_tree(ab));
+        if (lane == 0) part[t] = sum;
+    }
+}
+
+// ------------------------------------------------------------------------
 // host
 // ------------------------------------------------------------------------
 static int64_t ob_tiles(int64_t cs) { return (cs + kObTile - 1) / kObTile; }
@@ -459,6 +628,17 @@ static void launch_ob_reduce(const uint8_t* in, int64_t co, int64_t cs, int p, t
                chunk, seg, part);
 }
 
+template <typename T, int PMAX>
+static void launch_ob_reduce_lut(const uint8_t* in, int64_t co, int64_t cs, int p, int average,
+                                 typename T::storage* chunk, uint8_t* seg, float* part, int blocks, hipStream_t s) {
+    if (chunk)
+        launch(onebit_reduce_encode_lut_kernel<T, PMAX, true>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
+               average, chunk, seg, part);
+    else
+        launch(onebit_reduce_encode_lut_kernel<T, PMAX, false>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
+               average, chunk, seg, part);
+}
+
 template <typename T>
 static int ob_reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, void* tensor,
                                      int average, uint8_t* out, size_t out_bytes, int target, void* ws,
@@ -474,7 +654,19 @@ static int ob_reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int
     S* chunk = tensor ? static_cast<S*>(tensor) + (int64_t)target * cs : nullptr;  // nullptr: not stored
     float* part = static_cast<float*>(ws);
     uint8_t* seg = out + (int64_t)target * co;
-    if (tiles > 0) {
+    static const bool lut_on = [] {  // BAGUA_ONEBIT_LUT=0: the per-element tree kernel (A/B)
+        const char* v = std::getenv("BAGUA_ONEBIT_LUT");
+        return !(v && v[0] == '0');
+    }();
+    if (tiles > 0 && lut_on) {
+        const int blocks = ob_blocks(tiles, 1);
+        if (p <= 2)
+            launch_ob_reduce_lut<T, 2>(recv, co_in, cs, p, average, chunk, seg, part, blocks, s);
+        else if (p <= 8)
+            launch_ob_reduce_lut<T, 8>(recv, co_in, cs, p, average, chunk, seg, part, blocks, s);
+        else
+            launch_ob_reduce_lut<T, 16>(recv, co_in, cs, p, average, chunk, seg, part, blocks, s);
+    } else if (tiles > 0) {
         const int blocks = ob_blocks(tiles, 1);
         switch (reduce_by(p)) {
             case 2:
