@@ -118,3 +118,40 @@ def test_level3_tree_maximum_chunk(bc, oracle_c):
     del x
     want = oracle_compress(oracle_c, xh, F32, n, n, 1)
     assert np.array_equal(got.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("average", [1, 0])
+@pytest.mark.parametrize("p", list(range(1, 17)))
+def test_reduce_requantize_every_p(bc, oracle_c, dtype, average, p):
+    """The 1-bit fused middle step (onebit_reduce_encode_lut_kernel: p <= 2 direct
+    index, p <= 8 one 2^p table, 9 <= p <= 16 two half-tree tables) for every p and
+    both reductions: the re-encoded target segment equals the oracle's
+    decompress -> reduce_{mean,sum} -> compress(target), and the stored reduced
+    chunk equals the oracle's reduced chunk.  cs is ragged (last tile partial)."""
+    from oracle import oracle_np as NP
+    K = bc._native.K
+    cs = 1024 * 37 + 300
+    target = p // 2
+    rng = np.random.default_rng(1000 + 10 * p + average + dtype)
+    x = NP.from_f32((rng.standard_normal(p * cs) * 1e-3 * (1 + rng.random(p * cs))).astype(np.float32), dtype)
+    recv = oracle_compress(oracle_c, x, dtype, p * cs, cs, p)  # p segments, one scale each
+    t = np.zeros_like(x)
+    oracle_c.decompress_onebit(recv, p, t, dtype)
+    oracle_c.reduce_chunks(t, dtype, p, target, bool(average))
+    want = oracle_c.compress_onebit(t, dtype, p, target)
+    S = recv.size
+    co = S // p
+    rd = torch.from_numpy(recv.copy()).cuda()
+    out = torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
+    td = torch.zeros(p * cs, dtype=torch.float32 if dtype == F32 else torch.bfloat16, device="cuda")
+    wsb = K.bagua_onebit_workspace_bytes(cs, 1)
+    ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+    rc = K.bagua_onebit_reduce_requantize(dtype, rd.data_ptr(), S, cs, p, td.data_ptr(), average, out.data_ptr(), S,
+                                          target, ws.data_ptr(), wsb, None)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    g = out.cpu().numpy()
+    assert np.array_equal(g[target * co:(target + 1) * co], want[target * co:(target + 1) * co])
+    got_chunk = td.view(torch.int32 if dtype == F32 else torch.int16).cpu().numpy()[target * cs:(target + 1) * cs]
+    assert np.array_equal(got_chunk.view(np.uint8), t[target * cs:(target + 1) * cs].view(np.uint8))
