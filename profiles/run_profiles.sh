@@ -50,3 +50,10 @@ echo "profiles written for $R"
 for e in 1048576 6553600 26214400; do
   timeout -k 10 120 python3 bench.py --workload allreduce --elements $e --steps 50 --no-decentralized > "$OUT/b_ar1_small_$e.json"
 done
+# the 1-bit op's fused middle step at p = 1..16 (table-driven kernel), 1 GiB bucket
+timeout -k 10 200 python3 bagua-core_amd/tools/onebit_reduce_probe.py > "$OUT/onebit_reduce_probe.json"
+# the N > 1 line rehearsed with 8 ranks on this one GPU over RCCL's socket transport
+# (code path only; times are socket-bound)
+BAGUA_BENCH_SHARED_GPU=1 NCCL_IB_DISABLE=1 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 \
+  --nproc-per-node=8 --master-addr=127.0.0.1 --master-port=29641 bench.py --gpus 8 --steps 3 --warmup 1 \
+  --elements 4194304 > "$OUT/b_ar8_shared.json"
