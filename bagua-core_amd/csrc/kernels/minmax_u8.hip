@@ -380,9 +380,33 @@ static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs
 // ---- pipelined all-reduce building blocks ---------------------------------
 // A chunk is cut into `pieces` element ranges of L = align(ceil(cs/pieces), 512)
 // elements (trailing ones may be empty).  Piece k's fused reduce writes its
-// `fused_blocks(L)` min/max partials to slot k of the workspace; the
-// requantise folds all of them, which is the same min/max as one pass.
+// `fused_blocks(longest piece)` min/max partials to slot k of the workspace;
+// the requantise folds all of them, which is the same min/max as one pass.
+//
+// BAGUA_PIPELINE_TAPER=1 (read per call; every piece user in the process reads
+// it alike): from 3 pieces on, the first and the last piece are half the size
+// of the others (weights 1, 2, ..., 2, 1; edges 512-aligned).  The pipelined
+// op's codec work before the first exchange (quantise piece 0) and after the
+// last one (dequantise the last piece) is then that of 2(pieces-1) pieces
+// with only `pieces` exchange groups.  Off by default; bench.py times it at
+// N > 1 beside the uniform split.
+static bool piece_taper() {
+    const char* v = getenv("BAGUA_PIPELINE_TAPER");
+    return v && v[0] == '1';
+}
+
 static void piece_range(int cs, int pieces, int k, int* b, int* e) {
+    if (pieces >= 3 && piece_taper()) {
+        const int64_t W = 2 * (int64_t)(pieces - 1);
+        auto edge = [&](int j) -> int {
+            const int64_t w = j == 0 ? 0 : (j >= pieces ? W : 2 * (int64_t)j - 1);
+            const int64_t x = ((int64_t)cs * w / W + 511) / 512 * 512;
+            return (int)(x < cs ? x : cs);
+        };
+        *b = edge(k);
+        *e = edge(k + 1);
+        return;
+    }
     const int64_t L = (((int64_t)cs + pieces - 1) / pieces + 511) / 512 * 512;
     const int64_t lo = (int64_t)k * L, hi = lo + L;
     *b = (int)(lo < cs ? lo : cs);
@@ -390,9 +414,13 @@ static void piece_range(int cs, int pieces, int k, int* b, int* e) {
 }
 
 static int piece_blocks(int cs, int pieces, int per_vec) {
-    int b, e;
-    piece_range(cs, pieces, 0, &b, &e);
-    return fused_blocks(e - b, per_vec);
+    int longest = 0;
+    for (int k = 0; k < pieces; ++k) {
+        int b, e;
+        piece_range(cs, pieces, k, &b, &e);
+        if (e - b > longest) longest = e - b;
+    }
+    return fused_blocks(longest, per_vec);
 }
 
 template <typename T>

@@ -531,6 +531,17 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     if world > 1 and not headline_fallback:
         for q in (2, 8):
             sweep[str(q)] = side(f"pieces_{q}", lambda q=q: compressed_step(q))
+
+        def tapered(q):
+            # first and last piece half size (BAGUA_PIPELINE_TAPER, minmax_u8.hip piece_range)
+            os.environ["BAGUA_PIPELINE_TAPER"] = "1"
+            try:
+                compressed_step(q)
+            finally:
+                os.environ.pop("BAGUA_PIPELINE_TAPER", None)
+
+        for q in (4, 5):
+            sweep[f"{q}_tapered"] = side(f"pieces_{q}_tapered", lambda q=q: tapered(q))
     t_f = side("fp32_allreduce", fp32_step)
     # the same all-reduce with the 1-bit sign+scale codec (this repo's extension:
     # N/8 wire bytes per phase instead of N), fused middle step

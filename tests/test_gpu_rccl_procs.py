@@ -82,6 +82,21 @@ def test_collectives(tmp_path, world):
     assert np.array_equal(outs[0]["reduce"].view(np.float32), total)
 
 
+def test_tapered_pieces_over_rccl(tmp_path, oracle_c, monkeypatch):
+    """BAGUA_PIPELINE_TAPER (first and last piece half size) in every rank process: the
+    pipelined MinMax op over real RCCL still equals the reference sequence."""
+    monkeypatch.setenv("BAGUA_PIPELINE_TAPER", "1")
+    world, cs = 4, 4 * 16384
+    rng = np.random.default_rng(77)
+    xs = [(rng.standard_normal(world * cs) * 1e-3).astype(np.float32) for _ in range(world)]
+    want = simulate.centralized_low_precision(oracle_c, xs, F32, True)
+    outs = run_procs(tmp_path, "centralized", world, {f"x{r}": x for r, x in enumerate(xs)},
+                     method="MinMaxUInt8", dtype=F32, pieces=5, repeat=2, average=1)
+    for r, o in enumerate(outs):
+        for rep in ("t0", "t1"):
+            assert np.array_equal(o[rep], want[r].view(np.uint8)), (r, rep)
+
+
 @pytest.mark.parametrize("world,method,dtype,cs,pieces,average", [
     (2, "MinMaxUInt8", F32, 3 * 65536, 3, 1),  # pipelined, 3 pieces per chunk
     (4, "MinMaxUInt8", F16, 4 * 4096, 2, 0),   # reduce_sum (average = False)
@@ -172,6 +187,7 @@ def test_bench_line_multirank(tmp_path, world, fail_headline):
         assert d["headline_fallback"]["headline"].startswith("unpieced") and d["pieces"] == 1, d
     else:
         assert "headline_fallback" not in d, d
+        assert set(d["pieces_sweep_ms_per_step"]) == {"2", "8", "4_tapered", "5_tapered"}, d
         assert all(v > 0 for v in d["pieces_sweep_ms_per_step"].values()), d["pieces_sweep_ms_per_step"]
     assert d["roofline"]["frac"] > 0
 
