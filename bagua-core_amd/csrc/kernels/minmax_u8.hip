@@ -51,7 +51,10 @@ __device__ __forceinline__ void fold(float f, uint32_t& lo, uint32_t& hi) {
 // ------------------------------------------------------------------------
 // pass 1: per-workgroup partial min/max of each active chunk
 // ------------------------------------------------------------------------
-template <typename T>
+// REV: the grid sweeps each chunk from its end to its start (min/max is
+// order-free), so what the Infinity Cache holds afterwards is the chunk's
+// beginning -- the piece the pipelined op quantises first
+template <typename T, bool REV = false>
 __global__ __launch_bounds__(kBlock) void minmax_partials_kernel(
     const typename T::storage* __restrict__ in, int64_t in_num_elem, int64_t cs, int target,
     uint2* __restrict__ partials) {
@@ -72,7 +75,9 @@ __global__ __launch_bounds__(kBlock) void minmax_partials_kernel(
     uint32_t hi = max_space(-T::init_max());
     constexpr int SUB = kPartialsSub;
     const int64_t stride = (int64_t)gridDim.x * kBlock * SUB;
-    for (int64_t base = (int64_t)blockIdx.x * kBlock * SUB; base < nvec; base += stride) {
+    const int64_t ntile = (nvec + kBlock * SUB - 1) / (kBlock * SUB);
+    for (int64_t fwd = (int64_t)blockIdx.x * kBlock * SUB; fwd < nvec; fwd += stride) {
+        const int64_t base = REV ? (ntile - 1) * kBlock * SUB - fwd : fwd;
         if (base + kBlock * SUB <= nvec) {  // full tile: SUB loads in flight per lane
             uint4 r[SUB];
 #pragma unroll
@@ -318,7 +323,8 @@ template <typename T>
 int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, int p, uint8_t* out,
                            int64_t out_bytes, int target, hipStream_t s);
 
-// stage bit 1: min/max partials pass; bit 2: quantise pass (3 = whole compress).
+// stage bit 1: min/max partials pass; bit 2: quantise pass (3 = whole compress);
+// bit 4: the partials pass sweeps each chunk backwards (with bit 1 only).
 // Both stages derive the same partials count from the same arguments.
 template <typename T>
 static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint8_t* out,
@@ -339,7 +345,10 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
         const int rc = resident_compress_impl<T>(input, in_num_elem, cs, p, out, (int64_t)out_bytes, target, s);
         if (rc != BAGUA_ERR_UNSUPPORTED) return rc;
     }
-    if (stages & 1)
+    if ((stages & 1) && (stages & 4))
+        launch(minmax_partials_kernel<T, true>, dim3(nblk, nact), dim3(kBlock), 0, s,
+                           static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, partials);
+    else if (stages & 1)
         launch(minmax_partials_kernel<T>, dim3(nblk, nact), dim3(kBlock), 0, s,
                            static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, partials);
     if (stages & 2)
@@ -519,7 +528,7 @@ int bagua_minmax_u8_decompress(int dtype, const uint8_t* input, size_t input_byt
 int bagua_minmax_u8_compress_stage(int stage, int dtype, const void* input, int input_num_element, int chunk_size,
                                    int num_chunks, uint8_t* output, size_t output_bytes, void* workspace,
                                    size_t workspace_bytes, int target_chunk, bagua_stream_t stream) {
-    if (stage != 1 && stage != 2) return BAGUA_ERR_INVALID_ARG;
+    if (stage != 1 && stage != 2 && stage != 5) return BAGUA_ERR_INVALID_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
     switch (dtype) {
         case BAGUA_DTYPE_F32:

@@ -296,7 +296,9 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
     HIP2(hipEventRecord(requantised, s0));
     HIP2(hipStreamWaitEvent(s1, requantised, 0));
     // 1. min/max of every chunk, then quantise + exchange piece by piece
-    TRY2(bagua_minmax_u8_compress_stage(1, dt, x, (int)t->num_elem, cs, p, sb, k.S, ws, ws_bytes, -1, s0));
+    // (backwards: the chunks' first pieces, quantised next, stay in the Infinity Cache)
+    TRY2(bagua_minmax_u8_compress_stage(env_int("BAGUA_PARTIALS_FORWARD", 0) ? 1 : 5, dt, x, (int)t->num_elem, cs, p,
+                                        sb, k.S, ws, ws_bytes, -1, s0));
     for (int q = 0; q < pieces; ++q) {
         int b, e;
         bagua_minmax_u8_piece_range(cs, pieces, q, &b, &e);

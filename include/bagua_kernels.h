@@ -68,7 +68,9 @@ int bagua_minmax_u8_compress(int dtype, const void* input, int input_num_element
 /* The two passes of bagua_minmax_u8_compress launched separately (stage 1:
  * per-workgroup min/max partials into `workspace`; stage 2: fold partials,
  * header, quantise).  Same arguments in both calls; used for per-kernel
- * timing and for overlapping the passes with other work. */
+ * timing and for overlapping the passes with other work.  Stage 5 is stage 1
+ * sweeping each chunk from its end to its start (same partials), so that the
+ * chunks' beginnings are what the Infinity Cache holds afterwards. */
 int bagua_minmax_u8_compress_stage(int stage, int dtype, const void* input, int input_num_element,
                                    int chunk_size, int num_chunks, uint8_t* output, size_t output_bytes,
                                    void* workspace, size_t workspace_bytes, int target_chunk,
