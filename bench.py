@@ -85,6 +85,10 @@ def parse():
     ap.add_argument("--copy-chunks", type=int, default=2,
                     help="host workload: pieces per H2D / D2H copy (1 = one copy each way per bucket)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the cpu_baseline leg")
+    ap.add_argument("--kernel-events-every", type=int, default=5,
+                    help="codec workloads: the dominant kernel records start/stop events on every N-th timed step")
+    ap.add_argument("--stream", choices=["own", "current"], default="own",
+                    help="codec workloads: launch on a stream of their own or on torch's current (null) stream")
     return ap.parse_args()
 
 
@@ -114,7 +118,10 @@ def bench_codec(args, onebit: bool = False):
     g = torch.Generator(device=dev).manual_seed(0x5EED)
     x = (torch.randn(n, device=dev, generator=g) * 1e-3).to(tdt)
     y = torch.empty_like(x)
-    stream = torch.cuda.current_stream(dev)
+    # the codec runs on a stream of its own (a communicator's stream, as in the
+    # comm ops), not on the null stream (--stream current: A/B)
+    stream = torch.cuda.Stream(device=dev) if args.stream == "own" else torch.cuda.current_stream(dev)
+    torch.cuda.synchronize()  # x was generated on the current stream
     sp = ctypes.c_void_p(stream.cuda_stream)
     if onebit:
         S = K.bagua_onebit_compressed_bytes(n, p)
@@ -201,14 +208,19 @@ def bench_codec(args, onebit: bool = False):
     per = [sum(pev[k][i][0].elapsed_time(pev[k][i][1]) for k in range(nprof)) / nprof for i in range(len(calls))]
     dom = max(range(len(calls)), key=lambda i: per[i])
     # timed region: K steps, wall clock between synchronisations; the dominant
-    # kernel of every step records its own start/stop events
-    ev = kernel_events(args.steps)
+    # kernel records its own start/stop events on every `--kernel-events-every`-th
+    # step (each recorded pair costs the step ~3 us of dispatch: A/B in
+    # profiles/r02_kernel_events_ab.jsonl), so its average launch duration is
+    # measured live over the timed region on a sample of its steps
+    every = max(1, args.kernel_events_every)
+    sampled = list(range(0, args.steps, every))
+    ev = kernel_events(len(sampled))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         for i, c in enumerate(calls):
-            if i == dom:
-                K.bagua_time_next_kernel(ev[k][0].cuda_event, ev[k][1].cuda_event)
+            if i == dom and k % every == 0:
+                K.bagua_time_next_kernel(ev[k // every][0].cuda_event, ev[k // every][1].cuda_event)
             rc = c()
             if rc:
                 raise RuntimeError(f"kernel launch failed: {N.STATUS.get(rc, rc)}")
@@ -216,7 +228,7 @@ def bench_codec(args, onebit: bool = False):
     wall = time.perf_counter() - t0
     ms = wall * 1e3 / args.steps
     value = esz * n / (ms * 1e-3) / GiB  # gradient bytes processed (4N fp32, 2N bf16)
-    dom_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    dom_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
     per[dom] = dom_ms
     achieved = alg[dom] / (per[dom] * 1e-3) / 1e9
     step_alg = sum(alg)
@@ -236,8 +248,8 @@ def bench_codec(args, onebit: bool = False):
                           "wall_us": round(ms * 1e3, 2),
                           "achieved_gbs": round(step_alg / (ms * 1e-3) / 1e9, 1),
                           "frac": round(step_alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-        "per_kernel_note": "kernel-recorded HIP events (hipExtLaunchKernel); dominant kernel over the timed region, "
-                           "others over the last warmup steps",
+        "per_kernel_note": "kernel-recorded HIP events (hipExtLaunchKernel); dominant kernel over the timed region "
+                           f"(every {every}th step: {len(sampled)} of {args.steps}), others over the last warmup steps",
         "encode_gib_s": round(esz * n / (sum(per[:-1]) * 1e-3) / GiB, 1),
         "decode_gib_s": round(esz * n / (per[-1] * 1e-3) / GiB, 1),
     }
@@ -247,6 +259,7 @@ def bench_codec(args, onebit: bool = False):
     if not args.no_cold:
         x2 = (torch.randn(n, device=dev, generator=g) * 1e-3).to(tdt)
         y2, comp2 = torch.empty_like(y), torch.empty_like(comp)
+        torch.cuda.synchronize()  # x2 was generated on the current stream
         calls2 = launches_for(x2.data_ptr(), y2.data_ptr(), comp2.data_ptr()) if launches_for else None
         if calls2 is not None:
             pairs = [calls, calls2]
