@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--no-decentralized", action="store_true", help="skip the config-5 side measurement (N > 1)")
     ap.add_argument("--no-cold", action="store_true",
                     help="codec workloads: skip the two-bucket alternating side line")
+    ap.add_argument("--host-buffers", type=int, default=2,
+                    help="host workload: buckets in flight in the overlapped mode (device buffers per stage)")
     ap.add_argument("--copy-chunks", type=int, default=2,
                     help="host workload: pieces per H2D / D2H copy (1 = one copy each way per bucket)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the cpu_baseline leg")
@@ -297,13 +299,14 @@ def bench_host(args):
     torch.cuda.set_device(dev)
     g = torch.Generator().manual_seed(0x5EED)
     src = (torch.randn(n, generator=g) * 1e-3).pin_memory()
-    dst = [torch.empty(n, pin_memory=True) for _ in range(2)]
-    x = [torch.empty(n, device=dev) for _ in range(2)]
-    y = [torch.empty(n, device=dev) for _ in range(2)]
+    nb = max(2, args.host_buffers)
+    dst = [torch.empty(n, pin_memory=True) for _ in range(nb)]
+    x = [torch.empty(n, device=dev) for _ in range(nb)]
+    y = [torch.empty(n, device=dev) for _ in range(nb)]
     S = K.bagua_minmax_u8_compressed_bytes(0, n, 1)
     wsb = K.bagua_minmax_u8_workspace_bytes(n, 1)
-    comp = [torch.empty(S, dtype=torch.uint8, device=dev) for _ in range(2)]
-    ws = [torch.empty(wsb, dtype=torch.uint8, device=dev) for _ in range(2)]
+    comp = [torch.empty(S, dtype=torch.uint8, device=dev) for _ in range(nb)]
+    ws = [torch.empty(wsb, dtype=torch.uint8, device=dev) for _ in range(nb)]
     s_in, s_cmp, s_out = (torch.cuda.Stream(device=dev) for _ in range(3))
 
     def codec(b, st):
@@ -323,9 +326,9 @@ def bench_host(args):
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / steps
 
-    ev_in = [torch.cuda.Event() for _ in range(2)]
-    ev_cmp = [torch.cuda.Event() for _ in range(2)]
-    ev_out = [torch.cuda.Event() for _ in range(2)]
+    ev_in = [torch.cuda.Event() for _ in range(nb)]
+    ev_cmp = [torch.cuda.Event() for _ in range(nb)]
+    ev_out = [torch.cuda.Event() for _ in range(nb)]
 
     chunks = max(1, args.copy_chunks)
 
@@ -345,12 +348,12 @@ def bench_host(args):
 
     def overlapped(steps):
         torch.cuda.synchronize()
-        for b in range(2):  # start with every buffer free
+        for b in range(nb):  # start with every buffer free
             ev_cmp[b].record(s_cmp)
             ev_out[b].record(s_out)
         t0 = time.perf_counter()
         for i in range(steps):
-            b = i % 2
+            b = i % nb
             s_in.wait_event(ev_cmp[b])       # x[b] consumed by the codec of bucket i-2
             with torch.cuda.stream(s_in):
                 h2d(b)
@@ -380,10 +383,11 @@ def bench_host(args):
     t_ser = serial(args.steps)
     t_ovl = overlapped(args.steps)
     torch.cuda.synchronize()
-    ok = torch.equal(dst[(args.steps - 1) % 2], y[(args.steps - 1) % 2].cpu())
+    ok = torch.equal(dst[(args.steps - 1) % nb], y[(args.steps - 1) % nb].cpu())
     value = 4.0 * n / t_ovl / GiB
     cfg = {"workload": f"minmax_uint8_encode_decode_{4 * n >> 20}MiB_fp32_bucket_host_resident", "bucket_elements": n,
-           "n_chunks": 1, "config_index": 2, "buffers": "pinned host fp32 in/out", "copy_pieces": chunks}
+           "n_chunks": 1, "config_index": 2, "buffers": "pinned host fp32 in/out", "copy_pieces": chunks,
+           "buckets_in_flight": nb}
     extra = {"serial_gib_s": round(4.0 * n / t_ser / GiB, 2), "serial_ms_per_bucket": round(t_ser * 1e3, 3),
              "overlapped_gib_s": round(value, 2), "h2d_gib_s": round(copy_rate(True, 5), 2),
              "d2h_gib_s": round(copy_rate(False, 5), 2), "result_copied_back_intact": bool(ok)}
