@@ -200,6 +200,8 @@ CORE_SIGNATURES = {
     "bagua_bucket_clear_ops": (_i32, [_vp]),
     "bagua_bucket_num_ops": (_i32, [_vp]),
     "bagua_bucket_mark_tensor_ready": (_i32, [_vp, ctypes.c_char_p, _u64]),
+    "bagua_bucket_mark_tensor_ready_desc": (_i32, [_vp, ctypes.c_char_p, _u64, _T]),
+    "bagua_bucket_refresh_tensor": (_i32, [_vp, ctypes.c_char_p, _T]),
     "bagua_bucket_ready_for_comm": (_i32, [_vp]),
     "bagua_bucket_reset_comm_ready": (_i32, [_vp]),
     "bagua_bucket_execute": (_i32, [_vp, _u64]),
@@ -207,6 +209,7 @@ CORE_SIGNATURES = {
     "bagua_comm_backend_destroy": (None, [_vp]),
     "bagua_comm_backend_register_ordered_buckets": (_i32, [_vp, ctypes.POINTER(_vp), _i32]),
     "bagua_comm_backend_mark_communication_ready": (_i32, [_vp, ctypes.c_char_p, _u64]),
+    "bagua_comm_backend_mark_communication_ready_desc": (_i32, [_vp, ctypes.c_char_p, _u64, _T]),
     "bagua_comm_backend_wait_pending_comm_ops": (_i32, [_vp, ctypes.POINTER(_i32)]),
     "bagua_comm_backend_failures": (_i32, [_vp]),
     "bagua_ring_exchange_ops": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),

@@ -52,6 +52,8 @@ class BaguaCommBackendPy:
                     seen.add(t.name())
                     ptrs.add(t.data_ptr())
         N.check(rc, "register_ordered_buckets")
+        for b in self._ordered:  # the native call waited for everything scheduled
+            b._release_retired()
         self._ordered = list(buckets)
         self._names = {t.name() for b in buckets for t in b.tensors()}
 
@@ -62,14 +64,18 @@ class BaguaCommBackendPy:
         name = tensor.name()
         if name not in self._names:
             raise RuntimeError(f"TensorError: tensor {name} is not registered in any bucket")
-        N.check(N.C.bagua_comm_backend_mark_communication_ready(self._handle, name.encode(),
-                                                               int(ready_cuda_event_ptr or 0)),
+        # the tensor's current storage goes with it (the reference reads data_ptr at run time)
+        raw = tensor.raw()
+        N.check(N.C.bagua_comm_backend_mark_communication_ready_desc(self._handle, name.encode(),
+                                                                    int(ready_cuda_event_ptr or 0), ctypes.byref(raw)),
                 "mark_communication_ready")
 
     def wait_pending_comm_ops(self) -> int:
         """lib.rs:321-337: wait for every scheduled op; returns how many finished."""
         n = ctypes.c_int(0)
         rc = N.C.bagua_comm_backend_wait_pending_comm_ops(self._handle, ctypes.byref(n))
+        for b in self._ordered:  # nothing scheduled is left to run: cleared ops may go now
+            b._release_retired()
         if rc:
             raise RuntimeError(f"comm op failed: {N.STATUS.get(rc, rc)} ({n.value} ops waited for)")
         return n.value

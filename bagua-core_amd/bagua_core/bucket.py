@@ -115,7 +115,13 @@ class BaguaBucketPy:
         self._handle = ctypes.c_void_p(handle)
         self.name = name
         self._tensors = list(tensors)
+        self._by_name = {t.name(): t for t in tensors}
         self._ops: list = []
+        # ops removed by clear_ops while a scheduled execution of this bucket may still
+        # hold their native copies (callback thunks, communicator handles): kept alive
+        # until the scheduler has run everything it scheduled (the reference's Arc
+        # clones, lib.rs:143-146) -- released by BaguaCommBackendPy.wait_pending_comm_ops
+        self._retired: list = []
 
     def __del__(self):
         h = getattr(self, "_handle", None)
@@ -137,7 +143,12 @@ class BaguaBucketPy:
 
     def clear_ops(self) -> None:
         N.check(N.C.bagua_bucket_clear_ops(self._handle), "clear ops")
+        self._retired.extend(self._ops)
         self._ops.clear()
+
+    def _release_retired(self) -> None:
+        """every scheduled execution has run: the cleared ops can go"""
+        self._retired.clear()
 
     def print_ops(self) -> None:
         print(self._ops)
@@ -176,6 +187,21 @@ class BaguaBucketPy:
         self._append(DecentralizedLowPrecisionSynchronous(comm, compression, weight, left_peer_weight,
                                                           right_peer_weight, intranode=intra))
 
+    # The full-precision decentralized ops (decentralized_full_precision_synchronous.rs,
+    # decentralized_full_precision_asynchronous.rs) carry no compression: outside the
+    # compressed-gradient path this package rebuilds.  Same signatures as
+    # bagua-core-py/src/lib.rs:408-426 and :453-467, so callers get a clear error.
+    def append_decentralized_synchronous_op(self, communicator_internode, communicator_intranode,
+                                            hierarchical: bool = False, peer_selection_mode: str = "all",
+                                            peer_weight: BaguaTensorPy = None) -> None:
+        raise NotImplementedError("append_decentralized_synchronous_op (full-precision decentralized op) is outside "
+                                  "the compressed-gradient path; use append_low_precision_decentralized_synchronous_op")
+
+    def append_decentralized_asynchronous_op(self, communicator_internode, communicator_intranode,
+                                             peer_selection_mode: str = "all", torch_stream: int = 0) -> None:
+        raise NotImplementedError("append_decentralized_asynchronous_op (full-precision asynchronous model "
+                                  "averaging) is outside the compressed-gradient path")
+
     @staticmethod
     def _communicators(internode, intranode, hierarchical):
         """BaguaCommunicator::new (communicators/mod.rs:348-383): (internode, None), or in
@@ -196,8 +222,18 @@ class BaguaBucketPy:
 
     # ---- readiness (datatypes/mod.rs:1256-1266, 793-813), by tensor name --------
     def mark_tensor_ready(self, tensor: BaguaTensorPy, ready_cuda_event_ptr: int = 0) -> None:
-        N.check(N.C.bagua_bucket_mark_tensor_ready(self._handle, tensor.name().encode(), int(ready_cuda_event_ptr)),
-                f"tensor {tensor.name()} is not in bucket {self.name}")
+        # the tensor's CURRENT storage (data_ptr read at run time, datatypes/mod.rs:775-791)
+        raw = tensor.raw()
+        N.check(N.C.bagua_bucket_mark_tensor_ready_desc(self._handle, tensor.name().encode(),
+                                                        int(ready_cuda_event_ptr), ctypes.byref(raw)),
+                f"tensor {tensor.name()} is not in bucket {self.name} (or changed dtype/device)")
+
+    def _refresh(self) -> None:
+        """re-read every tensor's storage (a .data / set_ swap after the bucket was built)"""
+        for t in self._tensors:
+            raw = t.raw()
+            N.check(N.C.bagua_bucket_refresh_tensor(self._handle, t.name().encode(), ctypes.byref(raw)),
+                    f"tensor {t.name()} changed dtype or device")
 
     def ready_for_comm(self) -> bool:
         return bool(N.C.bagua_bucket_ready_for_comm(self._handle))
@@ -209,5 +245,9 @@ class BaguaBucketPy:
     def execute_ops(self, stream_ptr: Optional[int] = None) -> None:
         """Run every op now on the bucket's communication tensor (the worker loop body,
         bagua-core-internal/src/lib.rs:241-246); synchronous like the reference
-        (datatypes/mod.rs:1062-1066).  stream_ptr None: the first op's communicator stream."""
+        (datatypes/mod.rs:1062-1066) unless an op's communicator is async (then it
+        returns once the work is queued).  stream_ptr: the stream the pack / copy-back
+        run on (None: the first op's communicator stream); the ops run on their
+        communicator's stream, ordered against it by events."""
+        self._refresh()
         N.check(N.C.bagua_bucket_execute(self._handle, int(stream_ptr or 0)), f"ops of bucket {self.name}")

@@ -132,9 +132,11 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
     constexpr int N = Vec<T>::N;
     const int cidx = kReverse ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
     const int c = target < 0 ? cidx : target;
+    // K:468-472: every element of the range is quantised with the chunk's
+    // parameters, also those at or past in_num_elem (only the min/max of pass 1
+    // is limited to the valid prefix, K:538-545); the input holds p*cs elements
+    (void)in_num_elem;
     const int64_t len = e1 - e0;
-    int64_t n = chunk_valid(in_num_elem, cs, c) - e0;  // valid elements of the range
-    n = n < 0 ? 0 : (n > len ? len : n);
     const S* src = in + (int64_t)c * cs + e0;
     uint8_t* seg = out + (int64_t)c * chunk_offset;
 
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
     const int a = common_alignment<T>((uintptr_t)src, (uintptr_t)payload);
     if (a < 0) {  // no common vector alignment: scalar path over the whole chunk
         for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < len; j += (int64_t)gridDim.x * kBlock)
-            payload[j] = (uint8_t)(j < n ? quant(T::to_f(src[j]), q) : 0u);
+            payload[j] = (uint8_t)quant(T::to_f(src[j]), q);
         return;
     }
     const int64_t j0 = a < len ? a : len;
@@ -189,10 +191,9 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
     const uint4* __restrict__ vsrc = reinterpret_cast<const uint4*>(src + j0);
     uint8_t* vdst = payload + j0;
     const int64_t ntiles = (nvec + kVecPerBlockTile - 1) / kVecPerBlockTile;
-    const bool all_valid = (n == len);  // elements past in_num_elem quantise to 0
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int64_t base = (kReverse ? (ntiles - 1 - t) : t) * kVecPerBlockTile;
-        if (all_valid && base + kVecPerBlockTile <= nvec) {
+        if (base + kVecPerBlockTile <= nvec) {
             // full tile: all loads issued before any is consumed
             uint4 r[kSubtiles];
 #pragma unroll
@@ -206,23 +207,18 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
             }
             continue;
         }
-        for (int k = 0; k < kSubtiles; ++k) {  // ragged last tile / partially valid chunk
+        for (int k = 0; k < kSubtiles; ++k) {  // ragged last tile
             const int64_t v = base + k * kBlock + threadIdx.x;
             if (v >= nvec) continue;
             float f[N];
             unpack16<T>(nt_load16(&vsrc[v]), f);
-            uint32_t b[N];
-            const int64_t jv = j0 + v * N;
-#pragma unroll
-            for (int i = 0; i < N; ++i) b[i] = (jv + i < n) ? quant(f[i], q) : 0u;
-            store_bytes<T>(vdst + v * N, b);
+            quant_store_vec<T>(f, q, vdst + v * N);
         }
     }
     if (blockIdx.x == 0) {
-        for (int64_t j = threadIdx.x; j < j0; j += kBlock)
-            payload[j] = (uint8_t)(j < n ? quant(T::to_f(src[j]), q) : 0u);
+        for (int64_t j = threadIdx.x; j < j0; j += kBlock) payload[j] = (uint8_t)quant(T::to_f(src[j]), q);
         for (int64_t j = j0 + nvec * N + threadIdx.x; j < len; j += kBlock)
-            payload[j] = (uint8_t)(j < n ? quant(T::to_f(src[j]), q) : 0u);
+            payload[j] = (uint8_t)quant(T::to_f(src[j]), q);
     }
 }
 

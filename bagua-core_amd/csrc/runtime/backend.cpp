@@ -66,17 +66,6 @@ namespace {
 
 using namespace bagua;
 
-bool contiguous(const BaguaBucketC* b) {
-    const size_t esz = bagua_dtype_bytes(b->tensors[0].t.dtype);
-    uint64_t cur = 0;
-    for (size_t i = 0; i < b->tensors.size(); ++i) {
-        const bagua_tensor_t& t = b->tensors[i].t;
-        if (i > 0 && t.ptr != cur) return false;
-        cur = t.ptr + t.num_elem_allocated * esz;
-    }
-    return true;
-}
-
 hipStream_t ops_stream(const std::vector<bagua_bucket_op_t>& ops) {
     for (const bagua_bucket_op_t& op : ops) {
         if (op.intranode) return op.intranode->stream;  // hierarchical: the node's stream (communicators/mod.rs:385-392)
@@ -146,48 +135,81 @@ std::vector<bagua_bucket_op_t> copy_ops(BaguaBucketC* b) {
     return b->ops;
 }
 
+std::vector<BucketTensor> copy_tensors(BaguaBucketC* b) {
+    std::lock_guard<std::mutex> g(b->mu);
+    return b->tensors;
+}
+
+// `to` waits for the work queued on `from` so far (nothing when they are the same stream)
+int order_after(hipStream_t to, hipStream_t from) {
+    if (to == from) return BAGUA_OK;
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return BAGUA_ERR_HIP;
+    const bool ok = hipEventRecord(e, from) == hipSuccess && hipStreamWaitEvent(to, e, 0) == hipSuccess;
+    (void)hipEventDestroy(e);  // released once the recorded work completes
+    return ok ? BAGUA_OK : BAGUA_ERR_HIP;
+}
+
 // get_communication_tensor + ops + Drop (datatypes/mod.rs:963-1070) with the
-// events and ops the bucket had when it was scheduled (lib.rs:143-146 clones the ops)
-int execute_bucket(BaguaBucketC* b, const std::vector<uint64_t>& events, const std::vector<bagua_bucket_op_t>& ops,
-                   hipStream_t s) {
-    if (b->tensors.empty()) return BAGUA_ERR_INVALID_ARG;
-    const bagua_tensor_t& first = b->tensors[0].t;
+// tensors, events and ops the bucket had when it was scheduled (lib.rs:143-146
+// clones the ops; the reference reads each tensor's data_ptr at run time, here
+// the descriptors refreshed by mark-ready / execute).  `s` carries the ready
+// waits, the pack and the copy-back; the ops run on their communicator's stream
+// `os`, ordered after the pack and before the copy-back.
+int execute_bucket(BaguaBucketC* b, const std::vector<BucketTensor>& tensors, const std::vector<uint64_t>& events,
+                   const std::vector<bagua_bucket_op_t>& ops, hipStream_t s) {
+    if (tensors.empty()) return BAGUA_ERR_INVALID_ARG;
+    const bagua_tensor_t& first = tensors[0].t;
     DeviceGuard guard(first.device_id);
     for (uint64_t ev : events)  // :969-980 the stream waits for every tensor's ready event
         if (hipStreamWaitEvent(s, (hipEvent_t)(uintptr_t)ev, 0) != hipSuccess) return BAGUA_ERR_HIP;
     if (ops.empty()) return BAGUA_OK;
+    hipStream_t os = ops_stream(ops);
+    if (!os) os = s;
     const bool async = ops_async(ops);
     const size_t esz = bagua_dtype_bytes(first.dtype);
     uint64_t total_alloc = 0, total = 0;
-    for (const BucketTensor& t : b->tensors) {
-        total_alloc += t.t.num_elem_allocated;
-        total += t.t.num_elem;
+    bool contig = true;
+    uint64_t cur = 0;
+    for (size_t i = 0; i < tensors.size(); ++i) {
+        const bagua_tensor_t& t = tensors[i].t;
+        total_alloc += t.num_elem_allocated;
+        total += t.num_elem;
+        if (i > 0 && t.ptr != cur) contig = false;
+        cur = t.ptr + t.num_elem_allocated * esz;
     }
     int rc = BAGUA_OK;
-    if (contiguous(b)) {
+    if (contig) {
+        if ((rc = order_after(os, s)) != BAGUA_OK) return rc;
         const bagua_tensor_t flat{first.ptr, total_alloc, total_alloc, first.dtype, first.device_id};
         for (const bagua_bucket_op_t& op : ops)
-            if ((rc = run_op(op, &flat, b->name.c_str(), s, async)) != BAGUA_OK) break;
-        return rc;
+            if ((rc = run_op(op, &flat, b->name.c_str(), os, async)) != BAGUA_OK) break;
+        const int rc2 = order_after(s, os);  // the caller's stream sees the results
+        return rc != BAGUA_OK ? rc : rc2;
     }
     // :999-1038 pack num_elements() of every tensor into a pool buffer on the stream
     PoolBuffer buf;
     if ((rc = buf.allocate(first.device_id, total_alloc * esz)) != BAGUA_OK) return rc;
     uint8_t* dst = buf.as<uint8_t>();
-    for (const BucketTensor& t : b->tensors) {
+    for (const BucketTensor& t : tensors) {
         const size_t bytes = t.t.num_elem * esz;
         if (bytes && hipMemcpyAsync(dst, (const void*)(uintptr_t)t.t.ptr, bytes, hipMemcpyDeviceToDevice, s) !=
                          hipSuccess)
             return BAGUA_ERR_HIP;
         dst += bytes;
     }
+    if ((rc = order_after(os, s)) != BAGUA_OK) return rc;  // the ops read the packed buffer
     const bagua_tensor_t flat{buf.ptr(), total, total_alloc, first.dtype, first.device_id};
     for (const bagua_bucket_op_t& op : ops)
-        if ((rc = run_op(op, &flat, b->name.c_str(), s, async)) != BAGUA_OK) break;
+        if ((rc = run_op(op, &flat, b->name.c_str(), os, async)) != BAGUA_OK) break;
     // :1043-1070 copy back, then wait for the stream (the buffer returns to the pool);
-    // async: the buffer returns to the pool behind the stream instead
+    // async: the buffer returns to the pool behind the stream instead.  Queued work
+    // of a failed op still writes the buffer: the copy-back is skipped, the buffer's
+    // release stays ordered behind both streams.
+    const int ord = order_after(s, os);
+    if (rc == BAGUA_OK) rc = ord;
     const uint8_t* src = buf.as<uint8_t>();
-    for (const BucketTensor& t : b->tensors) {
+    for (const BucketTensor& t : tensors) {
         const size_t bytes = t.t.num_elem * esz;
         if (rc == BAGUA_OK && bytes &&
             hipMemcpyAsync((void*)(uintptr_t)t.t.ptr, src, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
@@ -195,18 +217,20 @@ int execute_bucket(BaguaBucketC* b, const std::vector<uint64_t>& events, const s
         src += bytes;
     }
     if (async) {
-        const uint64_t sv = (uint64_t)(uintptr_t)s;
+        const uint64_t sv[2] = {(uint64_t)(uintptr_t)s, (uint64_t)(uintptr_t)os};
         const uint64_t p = buf.ptr();
         buf.release_to_caller();
-        (void)pool_free_after(p, &sv, 1);
+        (void)pool_free_after(p, sv, os == s ? 1 : 2);
         return rc;
     }
     const hipError_t e = hipStreamSynchronize(s);
-    return rc != BAGUA_OK ? rc : (e == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP);
+    const hipError_t e2 = os == s ? hipSuccess : hipStreamSynchronize(os);
+    return rc != BAGUA_OK ? rc : (e == hipSuccess && e2 == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP);
 }
 
 struct Scheduled {
     BaguaBucketC* bucket = nullptr;
+    std::vector<BucketTensor> tensors;     // tensor descriptors at scheduling time
     std::vector<uint64_t> events;          // ready events at scheduling time
     std::vector<bagua_bucket_op_t> ops;    // the bucket's ops at scheduling time
     bool done = false;                     // executed (sync) / enqueued (async)
@@ -263,14 +287,17 @@ struct BaguaCommBackendC {
                 current_start = std::chrono::steady_clock::now();
             }
             hipStream_t s = ops_stream(item->ops);
-            const int rc = execute_bucket(item->bucket, item->events, item->ops, s);
+            const int rc = execute_bucket(item->bucket, item->tensors, item->events, item->ops, s);
             hipEvent_t fin = nullptr;
-            if (async && rc == BAGUA_OK) {
+            if (async) {
+                // also after a failed op: its bucket's earlier work may still be queued, and
+                // wait_pending_comm_ops must not return before it drained
                 {
                     std::lock_guard<std::mutex> lk(mu);
                     fin = take_event();
                 }
                 if (fin && hipEventRecord(fin, s) != hipSuccess) fin = nullptr;
+                if (!fin && s) (void)hipStreamSynchronize(s);
             }
             {
                 std::lock_guard<std::mutex> lk(mu);
@@ -349,14 +376,42 @@ int bagua_bucket_num_ops(BaguaBucketC* b) {
 }
 
 int bagua_bucket_mark_tensor_ready(BaguaBucketC* b, const char* tensor_name, uint64_t ready_event) {
+    return bagua_bucket_mark_tensor_ready_desc(b, tensor_name, ready_event, nullptr);
+}
+
+namespace {
+// a tensor's current descriptor replaces the recorded one (the reference reads
+// data_ptr/numel from the torch tensor at run time, datatypes/mod.rs:775-791);
+// dtype and device may not change (datatypes/mod.rs:1079-1118).  Caller holds mu.
+int refresh_locked(BucketTensor& t, const bagua_tensor_t* cur) {
+    if (!cur) return BAGUA_OK;
+    if (cur->dtype != t.t.dtype || cur->device_id != t.t.device_id || cur->num_elem_allocated < cur->num_elem)
+        return BAGUA_ERR_INVALID_ARG;
+    t.t = *cur;
+    return BAGUA_OK;
+}
+}  // namespace
+
+int bagua_bucket_mark_tensor_ready_desc(BaguaBucketC* b, const char* tensor_name, uint64_t ready_event,
+                                        const bagua_tensor_t* current) {
     if (!b || !tensor_name) return BAGUA_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(b->mu);
-    for (const BucketTensor& t : b->tensors)
+    for (BucketTensor& t : b->tensors)
         if (t.name == tensor_name) {
+            const int rc = refresh_locked(t, current);
+            if (rc != BAGUA_OK) return rc;
             b->ready.insert(t.name);
             if (ready_event) b->events[t.name] = ready_event;
             return BAGUA_OK;
         }
+    return BAGUA_ERR_INVALID_ARG;
+}
+
+int bagua_bucket_refresh_tensor(BaguaBucketC* b, const char* tensor_name, const bagua_tensor_t* current) {
+    if (!b || !tensor_name || !current) return BAGUA_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(b->mu);
+    for (BucketTensor& t : b->tensors)
+        if (t.name == tensor_name) return refresh_locked(t, current);
     return BAGUA_ERR_INVALID_ARG;
 }
 
@@ -373,7 +428,7 @@ int bagua_bucket_execute(BaguaBucketC* b, uint64_t stream) {
     if (!b) return BAGUA_ERR_INVALID_ARG;
     const std::vector<bagua_bucket_op_t> ops = copy_ops(b);
     hipStream_t s = stream ? (hipStream_t)(uintptr_t)stream : ops_stream(ops);
-    return execute_bucket(b, take_events(b), ops, s);
+    return execute_bucket(b, copy_tensors(b), take_events(b), ops, s);
 }
 
 BaguaCommBackendC* bagua_comm_backend_create(size_t schedule_channel_cap, int device_id) {
@@ -456,13 +511,18 @@ int bagua_comm_backend_register_ordered_buckets(BaguaCommBackendC* be, BaguaBuck
 }
 
 int bagua_comm_backend_mark_communication_ready(BaguaCommBackendC* be, const char* tensor_name, uint64_t ready_event) {
+    return bagua_comm_backend_mark_communication_ready_desc(be, tensor_name, ready_event, nullptr);
+}
+
+int bagua_comm_backend_mark_communication_ready_desc(BaguaCommBackendC* be, const char* tensor_name,
+                                                     uint64_t ready_event, const bagua_tensor_t* current) {
     // lib.rs:300-319
     if (!be || !tensor_name) return BAGUA_ERR_INVALID_ARG;
     std::unique_lock<std::mutex> lk(be->mu);
     if (be->ordered.empty()) return BAGUA_ERR_INVALID_ARG;  // "ordered buckets not yet set in comm backend"
     auto it = be->mapping.find(tensor_name);
     if (it == be->mapping.end()) return BAGUA_ERR_INVALID_ARG;
-    int rc = bagua_bucket_mark_tensor_ready(it->second, tensor_name, ready_event);
+    int rc = bagua_bucket_mark_tensor_ready_desc(it->second, tensor_name, ready_event, current);
     if (rc != BAGUA_OK) return rc;
     while (be->ordered.front()->ready_for_comm()) {
         BaguaBucketC* b = be->ordered.front();
@@ -474,6 +534,7 @@ int bagua_comm_backend_mark_communication_ready(BaguaCommBackendC* be, const cha
         if (be->stop) return BAGUA_ERR_INVALID_ARG;
         auto item = std::make_shared<Scheduled>();
         item->bucket = b;
+        item->tensors = copy_tensors(b);
         item->events = take_events(b);
         item->ops = copy_ops(b);
         be->channel.push_back(item);

@@ -573,7 +573,12 @@ int ring_exchange_group(BaguaSingleCommunicatorC* c, const RingPlan& P, int g, u
     return rc ? rc : rc_end;
 }
 
-bool ring_multipath_enabled(int p) { return p >= kRingMinMultipath && env_int("BAGUA_RING_MULTIPATH", 1) != 0; }
+// Opt-in (BAGUA_RING_MULTIPATH=1): the only timing so far is RCCL's socket
+// transport between processes on one GPU, where multipath was 5.3x slower than
+// the direct exchange (profiles/r02_b_ar8_shared_gpu_rccl_socket.json); until an
+// xGMI node shows it faster, the default is the reference's direct exchange
+// (decentralized_low_precision_synchronous.rs:98-115).
+bool ring_multipath_enabled(int p) { return p >= kRingMinMultipath && env_int("BAGUA_RING_MULTIPATH", 0) != 0; }
 
 }  // namespace
 

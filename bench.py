@@ -35,13 +35,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "bagua-core_amd"))
 sys.path.insert(0, ROOT)
 
+# The hardware-queue count this process inherited (the GPU box exports 4) and the
+# one HIP will actually use: both go into every line ("hw_queues").
+HW_QUEUES_INHERITED = os.environ.get("GPU_MAX_HW_QUEUES")
 if int(os.environ.get("WORLD_SIZE", "1")) > 1:
     # N > 1: the pipelined ops overlap a side stream (RCCL pieces) with the codec
     # stream, and RCCL keeps internal streams of its own.  HIP maps streams onto
     # GPU_MAX_HW_QUEUES hardware queues round-robin (4 by default); two streams on
     # one queue serialise (profiles/r02_host_copy_ab.jsonl shows what that costs).
-    # 8 keeps the op's streams on queues of their own.  Set before HIP initialises.
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    # Set explicitly (not setdefault: an inherited 4 would win) before HIP
+    # initialises; BAGUA_BENCH_HW_QUEUES overrides (A/B at the box's 4).
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BAGUA_BENCH_HW_QUEUES", "8")
     if os.environ.get("BAGUA_BENCH_SHARED_GPU"):
         # rehearsal of the N > 1 line on a one-GPU box (tests/test_gpu_rccl_procs.py): every
         # rank on device 0, each its own "host" to RCCL (which refuses two ranks of one
@@ -283,7 +287,7 @@ def bench_codec(args, onebit: bool = False):
     cfg = {"workload": ("onebit_sign_scale" if onebit else "minmax_uint8") +
            f"_encode_decode_{esz * n >> 20}MiB_{args.dtype}_bucket", "bucket_elements": n, "n_chunks": p,
            "compressed_bytes": S, "config_index": 3 if onebit else 2}
-    return value, ms, roof, cfg, extra, x
+    return value, ms, roof, cfg, extra, (x, comp)
 
 
 def bench_host(args):
@@ -391,43 +395,105 @@ def bench_host(args):
     extra = {"serial_gib_s": round(4.0 * n / t_ser / GiB, 2), "serial_ms_per_bucket": round(t_ser * 1e3, 3),
              "overlapped_gib_s": round(value, 2), "h2d_gib_s": round(copy_rate(True, 5), 2),
              "d2h_gib_s": round(copy_rate(False, 5), 2), "result_copied_back_intact": bool(ok)}
-    return value, t_ovl * 1e3, None, cfg, extra
+    x[0].copy_(src)
+    codec(0, torch.cuda.current_stream(dev))
+    torch.cuda.synchronize()
+    return value, t_ovl * 1e3, None, cfg, extra, (x[0], comp[0])
 
 
-def cpu_baseline(args, sample_elems: int = 1 << 24):
-    """The reference's algorithm (C restatement, oracle/bagua_oracle.c) on the
-    host cores: encode+decode of a bounded sample of the same workload."""
-    import numpy as np
-    from oracle import oracle_c
-    lib_threads = oracle_c.num_threads()
-    rng = np.random.default_rng(0x5EED)
-    x = (rng.standard_normal(sample_elems) * 1e-3).astype(np.float32)
-    out = np.empty_like(x)
-    buf = oracle_c.compress_minmax_u8(x, 0, 1)
-    oracle_c.decompress_minmax_u8(buf, 1, out, 0)
+def host_info() -> dict:
+    """The host cores the CPU baseline ran on: the machine's CPU count, this
+    process's affinity mask, the CPU model and the OpenMP threads used."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"os_cpu_count": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": model}
+
+
+def _cpu_timed(fn, budget_s: float, max_reps: int = 100000):
+    fn()  # warm (page faults, OpenMP pool)
     reps, t0 = 0, time.perf_counter()
     while True:
-        oracle_c.compress_minmax_u8(x, 0, 1, out=buf)
-        oracle_c.decompress_minmax_u8(buf, 1, out, 0)
+        fn()
         reps += 1
         el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or reps >= 100000:
-            break
+        if el >= budget_s or reps >= max_reps:
+            return reps, el
+
+
+def cpu_codec_baseline(args, xdev, comp_dev, onebit: bool = False):
+    """The reference's algorithm (C restatement, oracle/bagua_oracle.c; the
+    reference has no CPU path) on the host cores, on the SAME bucket
+    the GPU encoded: encode+decode of x.cpu(), timed for about
+    --cpu-seconds.  As a by-product the GPU's compressed bytes of that bucket
+    are compared with the CPU's (`matches_gpu_bytes`)."""
+    import numpy as np
+    from oracle import oracle_c
+    threads = oracle_c.num_threads()
+    dcode, npdt = {torch.float32: (0, np.float32), torch.float16: (1, np.float16),
+                   torch.bfloat16: (2, np.uint16)}[xdev.dtype]
+    x = (xdev.view(torch.int16) if xdev.dtype == torch.bfloat16 else xdev).cpu().numpy().view(npdt)
+    out = np.empty_like(x)
+    comp = oracle_c.compress_onebit(x, dcode, 1) if onebit else oracle_c.compress_minmax_u8(x, dcode, 1)
+    same = bool(np.array_equal(comp, comp_dev.cpu().numpy())) if comp_dev is not None else None
+
+    def step():
+        if onebit:
+            oracle_c.compress_onebit(x, dcode, 1, out=comp)
+            oracle_c.decompress_onebit(comp, 1, out, dcode)
+        else:
+            oracle_c.compress_minmax_u8(x, dcode, 1, out=comp)
+            oracle_c.decompress_minmax_u8(comp, 1, out, dcode)
+
+    reps, el = _cpu_timed(step, args.cpu_seconds)
     # config 1: 4 MiB fp32, the whole centralized op sequence (compress -> alltoall ->
     # decompress -> reduce -> compress -> allgather -> decompress) at p = 1 on the CPU path
     from oracle import simulate
+    rng = np.random.default_rng(0x5EED)
     x1 = [(rng.standard_normal(1 << 20) * 1e-3).astype(np.float32)]
-    simulate.centralized_low_precision(oracle_c, x1, 0, True)
-    r1, t1 = 0, time.perf_counter()
-    while time.perf_counter() - t1 < 1.0:
-        simulate.centralized_low_precision(oracle_c, x1, 0, True)
-        r1 += 1
-    cfg1 = round(4.0 * (1 << 20) * r1 / (time.perf_counter() - t1) / GiB, 3)
-    return {"value": round(4.0 * sample_elems * reps / el / GiB, 3), "unit": "GiB/s", "cores": lib_threads,
-            "config1_loopback_op_gib_s": cfg1,
-            "kind": "port",
-            "sample": f"{4 * sample_elems >> 20} MiB fp32 N(0,1e-3^2) bucket, MinMax-UInt8 encode+decode x{reps} "
-                      f"({el:.1f} s wall, {lib_threads} OpenMP threads, oracle/bagua_oracle.c)"}
+    r1, e1 = _cpu_timed(lambda: simulate.centralized_low_precision(oracle_c, x1, 0, True), 1.0)
+    codec = "1-bit sign+scale" if onebit else "MinMax-UInt8"
+    return {"value": round(x.nbytes * reps / el / GiB, 3), "unit": "GiB/s", "cores": threads,
+            "kind": "port", "host": host_info(), "matches_gpu_bytes": same,
+            "config1_loopback_op_gib_s": round(4.0 * (1 << 20) * r1 / e1 / GiB, 3),
+            "sample": f"the same {x.nbytes >> 20} MiB bucket the GPU encoded (x.cpu()), {codec} encode+decode "
+                      f"x{reps} ({el:.1f} s wall, {threads} OpenMP threads, oracle/bagua_oracle.c)"}
+
+
+def cpu_allreduce_baseline(args, world: int, n: int, dev, sample_elems: int = 1 << 22):
+    """The compressed centralized all-reduce (centralized_low_precision_synchronous.rs:30-71)
+    on the host cores: oracle/simulate.py composes the C restatement in the
+    reference's op order for all `world` ranks (collectives = array moves).
+    Inputs: the first `sample_elems` elements of every rank's own bucket
+    (torch.randn, seed 0x5EED + r, regenerated here), a bounded sample of the
+    same workload.  value = gradient bytes of all ranks / wall time."""
+    import numpy as np
+    from oracle import oracle_c, simulate
+    threads = oracle_c.num_threads()
+    m = min(n, sample_elems)
+    m -= m % world
+    xs = []
+    for r in range(world):
+        g = torch.Generator(device=dev).manual_seed(0x5EED + r)
+        xs.append((torch.randn(n, device=dev, generator=g) * 1e-3)[:m].cpu().numpy())
+    torch.cuda.empty_cache()
+    reps, el = _cpu_timed(lambda: simulate.centralized_low_precision(oracle_c, xs, 0, True),
+                          args.cpu_seconds, max_reps=10000)
+    return {"value": round(world * 4.0 * m * reps / el / GiB, 3), "unit": "GiB/s", "cores": threads,
+            "kind": "port", "host": host_info(),
+            "sample": f"{world} ranks x the first {4 * m >> 20} MiB of each rank's fp32 bucket (seed 0x5EED + r), "
+                      f"the whole MinMax-UInt8 op sequence for all ranks x{reps} ({el:.1f} s wall, {threads} OpenMP "
+                      "threads, oracle/simulate.py over oracle/bagua_oracle.c; rank 0 after the timed region)"}
 
 
 # ----------------------------------------------------------------- N > 1 ------
@@ -489,21 +555,35 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         # side measurements must not cost the headline line: an error that every rank
         # raises alike (argument checks, an unsupported shape) is recorded instead, and a
         # measurement that has not finished after SIDE_TIMEOUT_S aborts the communicator
-        # (ncclCommAbort: pending collectives return) so the line is still printed
+        # (ncclCommAbort: pending collectives return) so the line is still printed; the
+        # ranks then agree (gloo) to rebuild it, so the later side lines still measure
+        nonlocal comm
+        expired = []
+
         def expire():
-            side_errors[name] = f"timed out after {SIDE_TIMEOUT_S} s; communicator aborted"
+            expired.append(True)
+            side_errors[name] = f"timed out after {SIDE_TIMEOUT_S} s; communicator aborted and rebuilt"
             comm.abort()
 
         timer = threading.Timer(SIDE_TIMEOUT_S, expire)
         timer.daemon = True
         timer.start()
+        res = float("nan")
         try:
-            return timed(fn, max(3, args.steps // 2), max(1, args.warmup // 2))
+            res = timed(fn, max(3, args.steps // 2), max(1, args.warmup // 2))
         except Exception as e:  # noqa: BLE001
             side_errors.setdefault(name, str(e)[:200])
-            return float("nan")
         finally:
             timer.cancel()
+        flag = torch.tensor([1.0 if expired else 0.0])
+        if world > 1:
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if flag.item():
+            if not expired:
+                comm.abort()  # another rank's timer fired: every rank leaves the old communicator
+            comm = make_comm()
+            return float("nan")
+        return res
 
     # The headline: the pipelined op.  Its multi-group RCCL schedule has run over the
     # loopback transport, gloo and single-rank RCCL only; should it not
@@ -596,22 +676,23 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
                     comm.handle, *[ctypes.byref(r) for r in draws], N.COMPRESSION_MINMAX_UINT8, pieces),
                     "decentralized")
 
-            def direct(fn):
-                # the reference's exchange: the whole payload straight to both ring peers
-                os.environ["BAGUA_RING_MULTIPATH"] = "0"
+            def multipath_on(fn):
+                # opt-in relayed exchange (comm_ops.cpp ring_ops): 3/p of each piece direct,
+                # the rest through the other ranks; the default is the reference's direct one
+                os.environ["BAGUA_RING_MULTIPATH"] = "1"
                 try:
                     fn()
                 finally:
                     os.environ.pop("BAGUA_RING_MULTIPATH", None)
 
             multipath = world >= 6  # comm_ops.cpp kRingMinMultipath
-            t_dd = side("decentralized_direct", lambda: direct(dec_step)) if multipath else float("nan")
             t_d = side("decentralized", dec_step)
+            t_dm = side("decentralized_multipath", lambda: multipath_on(dec_step)) if multipath else float("nan")
             t_du = side("decentralized_unpieced", lambda: dec_step(1))
             decentralized = {"config_index": 5, "elements_per_rank": nb, "dtype": "bf16",
-                             "exchange": "multipath (3/p direct, the rest relayed)" if multipath else "direct",
+                             "exchange": "direct (the reference's; multipath is opt-in)",
                              "ms_per_step": round(t_d * 1e3, 3), "unpieced_ms_per_step": round(t_du * 1e3, 3),
-                             "direct_exchange_ms_per_step": round(t_dd * 1e3, 3) if multipath else None,
+                             "multipath_exchange_ms_per_step": round(t_dm * 1e3, 3) if multipath else None,
                              "gib_s_per_rank": round(2.0 * nb / t_d / GiB, 2),
                              "gib_s_total": round(world * 2.0 * nb / t_d / GiB, 2)}
             del bufs, draws
@@ -775,18 +856,28 @@ def main():
         workload = "codec" if world == 1 else "allreduce"
     cpu = None
     if workload in ("codec", "onebit"):
-        value, ms, roof, cfg, extra, _ = bench_codec(args, onebit=(workload == "onebit"))
-        if rank == 0 and world == 1 and not args.no_cpu_baseline and workload == "codec":
-            cpu = cpu_baseline(args)
+        value, ms, roof, cfg, extra, (xb, cb) = bench_codec(args, onebit=(workload == "onebit"))
+        if rank == 0 and not args.no_cpu_baseline:
+            cpu = cpu_codec_baseline(args, xb, cb, onebit=(workload == "onebit"))
+        del xb, cb
         dtype = f"{args.dtype} -> u8" if workload == "codec" else f"{args.dtype} -> 1bit"
     elif workload == "host":
-        value, ms, roof, cfg, extra = bench_host(args)
-        dtype = "f32 -> u8"
-    elif workload == "backend":
-        value, ms, roof, cfg, extra = bench_backend(args, world, rank, local_rank)
+        value, ms, roof, cfg, extra, (xb, cb) = bench_host(args)
+        if rank == 0 and not args.no_cpu_baseline:
+            cpu = cpu_codec_baseline(args, xb, cb)
+        del xb, cb
         dtype = "f32 -> u8"
     else:
-        value, ms, roof, cfg, extra = bench_allreduce(args, world, rank, local_rank)
+        if workload == "backend":
+            value, ms, roof, cfg, extra = bench_backend(args, world, rank, local_rank)
+            n_cpu = cfg["bucket_elements"]
+        else:
+            value, ms, roof, cfg, extra = bench_allreduce(args, world, rank, local_rank)
+            n_cpu = cfg["bucket_elements"]
+        # after every rank's timed region: rank 0 times the op on the host cores while
+        # the others wait at the closing barrier
+        if rank == 0 and not args.no_cpu_baseline:
+            cpu = cpu_allreduce_baseline(args, world, n_cpu, torch.device("cuda", local_rank))
         dtype = "f32 -> u8"
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
@@ -794,7 +885,8 @@ def main():
                 "vs_baseline": None, "dtype": dtype,
                 "data": "synthetic fp32 gradients N(0, 1e-3^2) (torch.randn, seed 0x5EED + rank), " +
                         ("in pinned host memory (H2D + D2H timed)" if workload == "host" else "resident in HBM"),
-                "config": cfg, "roofline": roof, "cpu_baseline": cpu}
+                "config": cfg, "roofline": roof, "cpu_baseline": cpu,
+                "hw_queues": {"inherited": HW_QUEUES_INHERITED, "effective": os.environ.get("GPU_MAX_HW_QUEUES")}}
         line.update(extra)
         print(json.dumps(_finite(line)), file=json_out, flush=True)
     if world > 1:

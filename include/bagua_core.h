@@ -188,7 +188,7 @@ int bagua_decentralized_low_precision_pipelined(BaguaSingleCommunicatorC* comm, 
 /* Ring exchange schedule of the fused decentralized op (host-only, no device work).
  * The reference sends the whole compressed bucket straight to both ring peers
  * (decentralized_low_precision_synchronous.rs:98-115), which loads 2 of a
- * GPU's 7 xGMI links.  From nranks >= 6 (BAGUA_RING_MULTIPATH=0 disables) each
+ * GPU's 7 xGMI links.  Opt-in (BAGUA_RING_MULTIPATH=1, from nranks >= 6), each
  * piece's bytes are cut into nranks slices: 3 go straight to the peer, slice k
  * (3 <= k < nranks) is relayed through rank +-(k-1), so every link carries at
  * most 4/nranks of the payload (8 ranks: half) instead of all of it; the relay
@@ -270,11 +270,22 @@ int bagua_bucket_num_ops(BaguaBucketC* bucket);
 /* readiness by tensor name (datatypes/mod.rs:793-813, 1256-1266); the event (0 = none)
  * is waited for by the stream of the bucket's next execution */
 int bagua_bucket_mark_tensor_ready(BaguaBucketC* bucket, const char* tensor_name, uint64_t ready_event);
+/* the same, and `current` (non-NULL) replaces the tensor's recorded descriptor: the
+ * reference reads data_ptr / numel from the torch tensor at run time
+ * (datatypes/mod.rs:775-791), so a storage swapped after the bucket was created is
+ * followed.  dtype and device must not change (BAGUA_ERR_INVALID_ARG). */
+int bagua_bucket_mark_tensor_ready_desc(BaguaBucketC* bucket, const char* tensor_name, uint64_t ready_event,
+                                        const bagua_tensor_t* current);
+int bagua_bucket_refresh_tensor(BaguaBucketC* bucket, const char* tensor_name, const bagua_tensor_t* current);
 int bagua_bucket_ready_for_comm(BaguaBucketC* bucket);
 int bagua_bucket_reset_comm_ready(BaguaBucketC* bucket);
 /* run the bucket's ops now on its communication tensor (in place when the tensors are
- * back to back, else packed into a pool buffer and copied back, datatypes/mod.rs:963-1070);
- * stream 0 = the first op's communicator stream.  Synchronous. */
+ * back to back, else packed into a pool buffer and copied back, datatypes/mod.rs:963-1070).
+ * `stream` (0 = the first op's communicator stream) carries the ready-event waits, the pack
+ * and the copy-back; the ops run on their communicator's stream, ordered after the pack
+ * and before the copy-back by events.  Synchronous (returns after both streams drained)
+ * unless an op's communicator is async (bagua_comm_set_async): then it returns once the
+ * work is queued. */
 int bagua_bucket_execute(BaguaBucketC* bucket, uint64_t stream);
 
 BaguaCommBackendC* bagua_comm_backend_create(size_t schedule_channel_cap, int device_id);
@@ -286,6 +297,10 @@ int bagua_comm_backend_register_ordered_buckets(BaguaCommBackendC* backend, Bagu
 /* lib.rs:300-319 (the tensor by name) */
 int bagua_comm_backend_mark_communication_ready(BaguaCommBackendC* backend, const char* tensor_name,
                                                uint64_t ready_event);
+/* the same with the tensor's current descriptor (see bagua_bucket_mark_tensor_ready_desc);
+ * a scheduled bucket runs with the descriptors it had when it was scheduled */
+int bagua_comm_backend_mark_communication_ready_desc(BaguaCommBackendC* backend, const char* tensor_name,
+                                                    uint64_t ready_event, const bagua_tensor_t* current);
 /* lib.rs:321-337: *completed = ops waited for; returns the first failure's status */
 int bagua_comm_backend_wait_pending_comm_ops(BaguaCommBackendC* backend, int* completed);
 /* ops the monitor saw running longer than 300 s (lib.rs:255-265) */

@@ -242,11 +242,16 @@ int orc_compress_minmax_u8(const void* in, int dtype, int in_num_elem, int chunk
         store_raw(seg + esz, dtype, mx);
         qparams q = make_qparams(load_raw(seg, dtype), load_raw(seg + esz, dtype));
         uint8_t* payload = seg + 32; /* K:470 */
+        /* K:468-472: EVERY element i < chunk_size of the chunk is quantised
+         * with the chunk's parameters -- including elements at or past
+         * in_num_elem, which only the min/max (K:541, min(remaining, cs))
+         * leaves out.  The input must hold num_chunks*chunk_size elements
+         * (DT:327: chunk_size = num_elements_allocated / n_chunks). */
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static)
 #endif
         for (int64_t j = 0; j < chunk_size; ++j)
-            payload[j] = j < n_c ? quant(load_f(src, dtype, j), q) : 0;
+            payload[j] = quant(load_f(src, dtype, j), q);
         /* slack after the payload: zero (reference: uninitialised) */
         memset(seg + 32 + chunk_size, 0, chunk_offset - 32 - (size_t)chunk_size);
     }

@@ -88,8 +88,11 @@ def minmax(x: np.ndarray, dtype: int) -> tuple[float, float]:
 def compress_minmax_u8(x: np.ndarray, dtype: int, n_chunks: int, target_chunk: int = -1,
                        out: np.ndarray | None = None, num_elem: int | None = None) -> np.ndarray:
     """BaguaTensor.compress("MinMaxUInt8", n_chunks, target_chunk) on a host array.
-    `num_elem` (default x.size) is the tensor's num_elements(): elements past it
-    are not part of the min/max and quantise to 0 (DT:339, K:455-479)."""
+    `num_elem` (default x.size) is the tensor's num_elements() (DT:339): elements
+    past it are left out of the chunk's min/max (K:538-545, min(remaining, cs))
+    but still quantised with that chunk's parameters (K:468-472 loops over every
+    i < chunk_size).  An empty chunk gets the init header (+-T_MAX) and, for
+    f32/bf16, scale = -0 and every byte 255 (decodes to NaN)."""
     assert x.size % n_chunks == 0, "compression tensor size % n_chunks must be 0"
     cs = x.size // n_chunks
     size = minmax_compressed_size(n_chunks, cs, dtype)

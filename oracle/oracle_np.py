@@ -110,8 +110,14 @@ def dequantize(q: np.ndarray, scale, lb) -> np.ndarray:
 
 
 def compress_minmax_u8(x: np.ndarray, dtype: int, n_chunks: int, target_chunk: int = -1,
-                       out: np.ndarray | None = None) -> np.ndarray:
-    """K:533-560 + K:455-479 (+ zeroed header gap / slack)."""
+                       out: np.ndarray | None = None, num_elem: int | None = None) -> np.ndarray:
+    """K:533-560 + K:455-479 (+ zeroed header gap / slack).
+
+    `num_elem` = the tensor's num_elements() (DT:339, default x.size).  The
+    host loop K:538-545 hands cub `min(remaining, chunk_size)` elements per
+    chunk (remaining may go negative: an empty range, header = init), while
+    the quantise kernel K:468-472 runs i over the whole chunk_size -- so the
+    elements past num_elem are outside the min/max but still quantised."""
     assert x.size % n_chunks == 0
     cs = x.size // n_chunks
     size = minmax_compressed_size(n_chunks, cs, dtype)
@@ -120,11 +126,14 @@ def compress_minmax_u8(x: np.ndarray, dtype: int, n_chunks: int, target_chunk: i
     co = size // n_chunks
     es = esize(dtype)
     xf = to_f32(x, dtype)
+    remaining = x.size if num_elem is None else int(num_elem)
     for c in range(n_chunks):
+        n_valid = max(0, min(remaining, cs))
+        remaining -= cs
         if target_chunk != -1 and c != target_chunk:
             continue
         seg = xf[c * cs:(c + 1) * cs]
-        mn, mx = minmax(seg, dtype)
+        mn, mx = minmax(seg[:n_valid], dtype)
         head = np.zeros(32, np.uint8)
         head[:es] = np.frombuffer(raw_bytes(mn, dtype), np.uint8)
         head[es:2 * es] = np.frombuffer(raw_bytes(mx, dtype), np.uint8)

@@ -18,7 +18,7 @@ import numpy as np
 
 def centralized_low_precision(backend, inputs: list[np.ndarray], dtype: int, average: bool = True,
                               method: str = "MinMaxUInt8", num_elem: int | None = None) -> list[np.ndarray]:
-    """`num_elem` < allocated size: the tensors' num_elements() (oracle_c MinMax only)."""
+    """`num_elem` < allocated size: the tensors' num_elements() (MinMax only; both backends)."""
     p = len(inputs)
     comp = backend.compress_minmax_u8 if method == "MinMaxUInt8" else backend.compress_onebit
     if num_elem is not None:

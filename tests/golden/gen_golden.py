@@ -156,9 +156,51 @@ def main() -> None:
             for nm, arrs in zip(("t", "w", "l", "r"), ra):
                 out[f"dec_out_{nm}_{dcase}"] = np.stack([a.view(np.uint8) for a in arrs])
             dcase += 1
-    out["counts"] = np.array([case, rcase, ocase, scase, dcase], np.int64)
+    # ---- partially valid tensors: num_elements() < num_elements_allocated -----------------
+    # K:538-545 limits each chunk's min/max to min(remaining, chunk_size) elements (an empty
+    # range when remaining <= 0: header = init), while K:468-472 quantises every element of
+    # every chunk with that chunk's parameters.  Both restatements must agree byte for byte.
+    pcase = 0
+    for dtype in DTYPES:
+        for p, cs, n_in, target in [(4, 1000, 3 * 1000 + 321, -1),  # last chunk ragged
+                                    (4, 1000, 2 * 1000, -1),        # last two chunks empty
+                                    (3, 517, 5, -1),                # first chunk holds 5 elements
+                                    (1, 4099, 0, -1),               # nothing valid at all
+                                    (5, 203, 4 * 203 - 10, 3),      # ragged target chunk
+                                    (5, 203, 4 * 203 - 10, 4),      # empty target chunk
+                                    (2, 1000, 1500, -1)]:
+            x = make_input("offset" if p == 2 else "n1e-3", p * cs, dtype, rng)
+            comp = C.compress_minmax_u8(x, dtype, p, target, num_elem=n_in)
+            assert same_bytes(comp, NP.compress_minmax_u8(x, dtype, p, target, num_elem=n_in)), \
+                ("minmax partial", p, cs, n_in, target, dtype)
+            dec = np.zeros_like(x)
+            if target == -1:
+                C.decompress_minmax_u8(comp, p, dec, dtype)
+                dn = np.zeros_like(x)
+                NP.decompress_minmax_u8(comp, p, dn, dtype)
+                assert same_bytes(dec, dn), ("decompress partial", p, cs, dtype)
+            out[f"mmp_in_{pcase}"] = x.view(np.uint8)
+            out[f"mmp_meta_{pcase}"] = np.array([dtype, p, cs, target, n_in], np.int64)
+            out[f"mmp_comp_{pcase}"] = comp
+            out[f"mmp_dec_{pcase}"] = dec.view(np.uint8)
+            pcase += 1
+    cpcase = 0
+    for dtype in (C.F32, C.BF16):
+        for p, cs, short in [(2, 1000, 37), (4, 999, 500), (3, 512, 517)]:
+            xs = [make_input("n1e-3", p * cs, dtype, rng) for _ in range(p)]
+            if (C.minmax_compressed_size(p, cs, dtype)) % p:
+                continue
+            ya = simulate.centralized_low_precision(C, xs, dtype, True, num_elem=p * cs - short)
+            yb = simulate.centralized_low_precision(NP, xs, dtype, True, num_elem=p * cs - short)
+            assert all(same_bytes(a, b) for a, b in zip(ya, yb)), ("centralized partial", p, dtype)
+            out[f"cenp_meta_{cpcase}"] = np.array([dtype, p, cs, p * cs - short], np.int64)
+            out[f"cenp_in_{cpcase}"] = np.stack([x.view(np.uint8) for x in xs])
+            out[f"cenp_out_{cpcase}"] = np.stack([y.view(np.uint8) for y in ya])
+            cpcase += 1
+    out["counts"] = np.array([case, rcase, ocase, scase, dcase, pcase, cpcase], np.int64)
     np.savez_compressed(OUT, **out)
-    print(f"wrote {OUT}: minmax {case}, reduce {rcase}, onebit {ocase}, centralized {scase}, decentralized {dcase}; "
+    print(f"wrote {OUT}: minmax {case}, reduce {rcase}, onebit {ocase}, centralized {scase}, decentralized {dcase}, "
+          f"partial minmax {pcase}, partial centralized {cpcase}; "
           f"{os.path.getsize(OUT)} bytes")
 
 

@@ -277,3 +277,84 @@ def test_scheduler_multirank_loopback(bc, oracle_c, p):
                 assert np.array_equal(got.view(np.uint32), want[r].view(np.uint32)), (it, b, r)
     assert all(s == [f"bucket{b}" for b in range(n_buckets)] * 2 for s in seen), seen
     del backends
+
+
+def test_clear_ops_while_a_python_op_is_queued(bc):
+    """clear_ops on a bucket that is scheduled but not yet run: the native item holds a
+    copy of the op (its ctypes thunk); the Python op must stay alive until the scheduler
+    has run it (the reference clones its ops into Arcs, lib.rs:143-146)."""
+    import gc
+    import time
+    gate = threading.Event()
+    seen = []
+    first = bc.BaguaBucketPy("first", [bc.BaguaTensorPy(torch.zeros(64, device="cuda"), "f0")])
+    first.append_python_op(lambda name: (gate.wait(10), seen.append(name)))  # holds the worker
+    second = bc.BaguaBucketPy("second", [bc.BaguaTensorPy(torch.zeros(64, device="cuda"), "s0")])
+    second.append_python_op(lambda name: seen.append(name))
+    backend = bc.BaguaCommBackendPy(4, 0)
+    backend.register_ordered_buckets([first, second])
+    backend.mark_communication_ready(first.tensors()[0], 0)
+    backend.mark_communication_ready(second.tensors()[0], 0)  # queued behind `first`
+    time.sleep(0.05)
+    second.clear_ops()  # the queued item still refers to the callback
+    gc.collect()
+    gate.set()
+    assert backend.wait_pending_comm_ops() == 2
+    assert seen == ["first", "second"], seen
+    assert second._retired == []  # released once everything scheduled has run
+    # the next iteration runs without the cleared op
+    backend.mark_communication_ready(first.tensors()[0], 0)
+    backend.mark_communication_ready(second.tensors()[0], 0)
+    assert backend.wait_pending_comm_ops() == 2
+    assert seen == ["first", "second", "first"], seen
+
+
+@pytest.mark.parametrize("via", ["scheduler", "execute"])
+def test_storage_swapped_after_bucket_creation(bc, comm, oracle_c, via):
+    """`t.data = other` after the bucket was built: the op must run on the tensor's
+    CURRENT storage (the reference reads data_ptr at run time, datatypes/mod.rs:775-791)
+    and leave the old storage alone."""
+    n = 3 * 40000
+    rng = np.random.default_rng(21)
+    x_old = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+    x_new = (rng.standard_normal(n) * 1e-3 + 0.25).astype(np.float32)
+    t = torch.from_numpy(x_old.copy()).cuda()
+    old_storage = t.data
+    bt = bc.BaguaTensorPy(t, f"swap_{via}")
+    bk = bc.BaguaBucketPy(f"swap_bucket_{via}", [bt])
+    bk.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+    t.data = torch.from_numpy(x_new.copy()).cuda()  # new storage, same tensor object
+    torch.cuda.synchronize()
+    if via == "scheduler":
+        backend = bc.BaguaCommBackendPy(2, 0)
+        backend.register_ordered_buckets([bk])
+        backend.mark_communication_ready(bt, 0)
+        assert backend.wait_pending_comm_ops() == 1
+    else:
+        bk.execute_ops()
+    torch.cuda.synchronize()
+    want = simulate.centralized_low_precision(oracle_c, [x_new], F32, True)[0]
+    assert np.array_equal(t.cpu().numpy().view(np.uint32), want.view(np.uint32))
+    assert np.array_equal(old_storage.cpu().numpy().view(np.uint32), x_old.view(np.uint32))
+
+
+def test_execute_on_a_foreign_stream_orders_the_pack(bc, comm, oracle_c):
+    """execute_ops(stream) with a stream other than the communicator's: the pack (on
+    `stream`, behind a long sleep there) must land before the op reads it, and the
+    copy-back after the op (event ordering in execute_bucket)."""
+    per = 3 * 30000
+    rng = np.random.default_rng(22)
+    h = (rng.standard_normal(per) * 1e-3).astype(np.float32)
+    parts = [torch.from_numpy(q.copy()).cuda() for q in np.array_split(h, 3)]
+    gaps = [torch.empty(4096, device="cuda") for _ in range(3)]  # noqa: F841 - scattered tensors
+    bk = bc.BaguaBucketPy("foreign", [bc.BaguaTensorPy(p, f"fp{i}") for i, p in enumerate(parts)])
+    bk.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(20_000_000)  # the pack waits behind this on `s`
+    bk.execute_ops(s.cuda_stream)
+    torch.cuda.synchronize()
+    want = simulate.centralized_low_precision(oracle_c, [h], F32, True)[0]
+    got = torch.cat(parts).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))

@@ -47,21 +47,33 @@ def test_default_run_is_config2_with_cpu_baseline():
     assert abs(d["value"] - 256 / 1024 / (d["ms_per_step"] * 1e-3)) < 0.01 * d["value"]
     assert d["roofline"]["kernel"] == "minmax_resident_encode_kernel"
     assert d["roofline"]["traffic"] and d["roofline"]["traffic"] > 0  # committed PMC summary
+    check_cpu(d)
+    # the CPU leg runs on the same 256 MiB bucket, and its bytes equal the GPU's
+    assert "256 MiB bucket" in d["cpu_baseline"]["sample"] and d["cpu_baseline"]["matches_gpu_bytes"] is True
+
+
+def check_cpu(d):
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+    h = c["host"]
+    assert h["os_cpu_count"] >= 1 and h["affinity_cpus"] >= 1 and "cpu_model" in h
+    assert d["hw_queues"]["effective"] == d["hw_queues"]["inherited"]  # N = 1 leaves the setting alone
 
 
 def test_onebit_run():
-    d = run_bench("--workload", "onebit", "--steps", "5", "--warmup", "2", "--no-cpu-baseline")
+    d = run_bench("--workload", "onebit", "--steps", "5", "--warmup", "2", "--cpu-seconds", "0.5")
     check_common(d, 5, 2)
     assert d["config"]["config_index"] == 3
     assert d["roofline"]["kernel"] == "onebit_encode_kernel"
+    check_cpu(d)
+    assert d["cpu_baseline"]["matches_gpu_bytes"] is True
 
 
 def test_allreduce_run_single_rank():
-    d = run_bench("--workload", "allreduce", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+    d = run_bench("--workload", "allreduce", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0.5",
                   "--no-decentralized", timeout=200)
     check_common(d, 3, 1)
+    check_cpu(d)
     assert d["config"]["config_index"] == 4 and d["config"]["parallelism"] == "dp1"
     assert d["fp32_allreduce_gib_s"] > 0 and d["onebit_allreduce"]["ms_per_step"] > 0
     assert "side_errors" not in d

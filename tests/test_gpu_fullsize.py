@@ -103,9 +103,10 @@ def test_centralized_onebit_allreduce_1gib_p8_properties():
     assert bool((torch.sign(y)[clear] == torch.sign(m)[clear]).all()), "sign of the reduced mean"
 
 
-def test_decentralized_ring_bf16_p8_full_size_properties():
-    """Config 5 at full size (2^27 bf16 elements per rank, 8 ranks; from 6 ranks the
-    exchange is multipath): with mix_r = t_r + (l_r + r_r) f13 + w_r f53 (f13, f53 =
+@pytest.mark.parametrize("multipath", ["0", "1"])
+def test_decentralized_ring_bf16_p8_full_size_properties(multipath):
+    """Config 5 at full size (2^27 bf16 elements per rank, 8 ranks; the default direct
+    exchange and the opt-in multipath one): with mix_r = t_r + (l_r + r_r) f13 + w_r f53 (f13, f53 =
     1/3 and -5/3 rounded to bf16 as the 16-bit addmul does; the bucket
     each rank quantises, decentralized_low_precision_synchronous.rs:45-64) and
     d_r its quantisation step, after the op
@@ -141,8 +142,17 @@ def test_decentralized_ring_bf16_p8_full_size_properties():
         N.check(N.C.bagua_decentralized_low_precision_synchronous(comms[r].handle, *[ctypes.byref(x) for x in raws],
                                                                   N.COMPRESSION_MINMAX_UINT8), f"rank {r}")
 
-    run_ranks(rank, p)
-    torch.cuda.synchronize()
+    import os
+    old_env = os.environ.get("BAGUA_RING_MULTIPATH")
+    os.environ["BAGUA_RING_MULTIPATH"] = multipath
+    try:
+        run_ranks(rank, p)
+        torch.cuda.synchronize()
+    finally:
+        if old_env is None:
+            os.environ.pop("BAGUA_RING_MULTIPATH", None)
+        else:
+            os.environ["BAGUA_RING_MULTIPATH"] = old_env
     for r in range(p):
         t_new = ts["t"][r].double()
         assert torch.equal(ts["w"][r].view(torch.int16), ts["t"][r].view(torch.int16)), f"rank {r}: w != t"

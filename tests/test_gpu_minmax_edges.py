@@ -63,3 +63,34 @@ def test_minmax_partial_buckets_vs_oracle(bc, oracle_c, dtype, p, cs, n_in, targ
     dw = np.empty(p * cs, dtype=STORAGE[dtype])
     oracle_c.decompress_minmax_u8(want, p, dw, dtype)
     assert_float_bits_equal(to_host(y, dtype), dw, dtype, "decode")
+
+
+def test_minmax_partial_goldens(bc, goldens):
+    """The committed partially valid cases (tests/golden/gen_golden.py, both
+    oracles agree): elements past input_num_element are outside the chunk's
+    min/max (K:538-545) but quantised with it (K:468-472); an empty chunk
+    carries the init header and bytes 255."""
+    K = bc._native.K
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for i in range(int(goldens["counts"][5])):
+        dtype, p, cs, target, n_in = (int(v) for v in goldens[f"mmp_meta_{i}"])
+        x = goldens[f"mmp_in_{i}"].view(STORAGE[dtype])
+        want = goldens[f"mmp_comp_{i}"]
+        S = K.bagua_minmax_u8_compressed_bytes(dtype, cs, p)
+        assert S == want.size
+        wsb = K.bagua_minmax_u8_workspace_bytes(cs, p)
+        ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+        out = torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
+        xd = to_dev(x, dtype)
+        assert K.bagua_minmax_u8_compress(dtype, xd.data_ptr(), n_in, cs, p, out.data_ptr(), S, ws.data_ptr(), wsb,
+                                          target, sp) == 0
+        got = out.cpu().numpy()
+        if target >= 0:
+            co = S // p
+            assert np.array_equal(got[target * co:(target + 1) * co], want[target * co:(target + 1) * co]), f"case {i}"
+            continue
+        assert np.array_equal(got, want), f"case {i}"
+        y = torch.empty(p * cs, dtype=xd.dtype, device="cuda")
+        assert K.bagua_minmax_u8_decompress(dtype, out.data_ptr(), S, cs, p, y.data_ptr(), sp) == 0
+        assert_float_bits_equal(to_host(y, dtype), goldens[f"mmp_dec_{i}"].view(STORAGE[dtype]), dtype,
+                                f"case {i} decode")

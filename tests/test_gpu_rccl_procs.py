@@ -163,8 +163,8 @@ def test_hierarchical(tmp_path, oracle_c):
 def test_bench_line_multirank(tmp_path, world, fail_headline):
     """bench.py's N > 1 line (config 4 + side lines) end to end under torch.distributed.run
     with `world` ranks on the one GPU (BAGUA_BENCH_SHARED_GPU): the pipelined headline must
-    not fall back, and the side measurements must not fail (8 ranks: the multipath ring
-    exchange and its direct-exchange side line).  fail_headline: the headline's communicator
+    not fall back, and the side measurements must not fail (8 ranks: the direct ring
+    exchange and the opt-in multipath side line).  fail_headline: the headline's communicator
     is aborted (BAGUA_BENCH_FAIL_HEADLINE, ncclCommAbort on every rank), so the line must come
     from the unpieced op on a fresh RCCL communicator, with every side line still measured."""
     import json
@@ -174,7 +174,7 @@ def test_bench_line_multirank(tmp_path, world, fail_headline):
         env["BAGUA_BENCH_FAIL_HEADLINE"] = "1"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={29517 + world + 20 * fail_headline}", os.path.join(ROOT, "bench.py"), "--gpus", str(world),
-           "--steps", "3", "--warmup", "1", "--elements", str(1 << 22)]
+           "--steps", "3", "--warmup", "1", "--elements", str(1 << 22), "--cpu-seconds", "1"]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -190,6 +190,10 @@ def test_bench_line_multirank(tmp_path, world, fail_headline):
         assert set(d["pieces_sweep_ms_per_step"]) == {"2", "8", "4_tapered", "5_tapered"}, d
         assert all(v > 0 for v in d["pieces_sweep_ms_per_step"].values()), d["pieces_sweep_ms_per_step"]
     assert d["roofline"]["frac"] > 0
+    # the CPU path beside every N: rank 0 runs the op sequence for all ranks on the host cores
+    c = d["cpu_baseline"]
+    assert c and c["value"] > 0 and c["cores"] >= 1 and c["host"]["os_cpu_count"] >= 1 and str(world) in c["sample"]
+    assert d["hw_queues"]["effective"] == "8", d["hw_queues"]
 
 
 def test_native_scheduler(tmp_path, oracle_c):
