@@ -28,7 +28,34 @@ int minmax_partials_blocks(int64_t cs, int per_vec, int nact, size_t ws_bytes); 
 // apply 455-487 -> 406-436 us and the op 1.02-1.05 -> 0.97-1.01 ms from U = 1 to
 // U = 4; the mix moves within noise)
 constexpr int kMixUnroll = 4;
-constexpr int kApplyUnroll = 4;
+
+// ring_apply variants (tools/ring_apply_sweep.py; BAGUA_RING_APPLY_CFG selects one,
+// read per call): vectors per tensor per batch, nt-store mask (bit 0 l, 1 r, 2 t,
+// 3 w), nt loads of l / r / w, contiguous ranges per workgroup, grid cap
+struct ApplyCfg {
+    int u, sp;
+    bool ntl, contig;
+    int max_blocks;
+};
+constexpr ApplyCfg kApplyCfg[] = {
+    {4, 0xF, false, false, 4096},  // 0: round 2 (nt stores, grid-strided)
+    {4, 0x0, false, false, 4096},  // 1: default-policy stores
+    {4, 0xC, false, false, 4096},  // 2: nt t / w, default l / r
+    {4, 0x3, false, false, 4096},  // 3: default t / w, nt l / r
+    {4, 0xF, true, false, 4096},   // 4: + nt loads
+    {2, 0xF, false, false, 4096},  // 5: U = 2
+    {4, 0xF, false, true, 4096},   // 6: contiguous ranges
+    {4, 0x0, true, false, 4096},   // 7: nt loads, default stores
+    {4, 0xF, false, true, 1024},   // 8: contiguous, 4 workgroups per CU
+    {4, 0xF, false, false, 1024},  // 9: grid-strided, 1024 workgroups
+};
+constexpr int kApplyNumCfg = (int)(sizeof(kApplyCfg) / sizeof(kApplyCfg[0]));
+constexpr int kApplyDefaultCfg = 0;
+static int apply_cfg() {
+    const char* e = getenv("BAGUA_RING_APPLY_CFG");
+    const int c = (e && *e) ? atoi(e) : kApplyDefaultCfg;
+    return c >= 0 && c < kApplyNumCfg ? c : kApplyDefaultCfg;
+}
 
 // K:236-244 addmul as the elementwise kernels compute it (elementwise.hip)
 template <typename T>
@@ -120,7 +147,22 @@ __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* _
     }
 }
 
-template <typename T, int U>
+// 16-B stores of the apply pass, per output: non-temporal or default policy
+template <bool NT>
+__device__ __forceinline__ void store16(const uint4& v, uint4* p) {
+    if constexpr (NT) nt_store16(v, p);
+    else *p = v;
+}
+template <bool NT>
+__device__ __forceinline__ uint4 load16(const uint4* p) {
+    if constexpr (NT) return nt_load16(p);
+    else return *p;
+}
+
+// SP: non-temporal store mask (bit 0 l, 1 r, 2 t, 3 w); NTL: non-temporal loads of
+// l / r / w; CONTIG: each workgroup sweeps one contiguous range instead of the
+// grid-strided loop (ring_apply variants, BAGUA_RING_APPLY_CFG, tools/ring_apply_sweep.py)
+template <typename T, int U, int SP, bool NTL, bool CONTIG>
 __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __restrict__ mine,
                                                             const uint8_t* __restrict__ from_left,
                                                             const uint8_t* __restrict__ from_right,
@@ -157,38 +199,55 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
             ft[i] = tm[bm[i]] + fw[i];   // t = dq(mine) + W
         }
         const uint4 ot = pack16<T>(ft);
-        nt_store16(pack16<T>(fl), reinterpret_cast<uint4*>(l) + v);
-        nt_store16(pack16<T>(fr), reinterpret_cast<uint4*>(r) + v);
-        nt_store16(ot, reinterpret_cast<uint4*>(t) + v);
-        nt_store16(ot, reinterpret_cast<uint4*>(w) + v);         // W = t (clone)
+        store16<(SP & 1) != 0>(pack16<T>(fl), reinterpret_cast<uint4*>(l) + v);
+        store16<(SP & 2) != 0>(pack16<T>(fr), reinterpret_cast<uint4*>(r) + v);
+        store16<(SP & 4) != 0>(ot, reinterpret_cast<uint4*>(t) + v);
+        store16<(SP & 8) != 0>(ot, reinterpret_cast<uint4*>(w) + v);  // W = t (clone)
     };
+    const uint4* l4 = reinterpret_cast<const uint4*>(l);
+    const uint4* r4 = reinterpret_cast<const uint4*>(r);
+    const uint4* w4 = reinterpret_cast<const uint4*>(w);
     auto one = [&](int64_t v) {
         uint32_t bm[N], bl[N], br[N];
         load_bytes<T>(pm + v * N, bm);
         load_bytes<T>(pl + v * N, bl);
         load_bytes<T>(pr + v * N, br);
-        body(v, bm, bl, br, reinterpret_cast<const uint4*>(l)[v], reinterpret_cast<const uint4*>(r)[v],
-             reinterpret_cast<const uint4*>(w)[v]);
+        body(v, bm, bl, br, load16<NTL>(l4 + v), load16<NTL>(r4 + v), load16<NTL>(w4 + v));
     };
-    // U vectors per tensor per iteration, all loads issued before any is consumed
-    for (int64_t v = e0 / N + (int64_t)blockIdx.x * kBlock + threadIdx.x; v < v1; v += stride * U) {
-        if (v + (U - 1) * stride < v1) {
-            uint32_t bm[U][N], bl[U][N], br[U][N];
-            uint4 rl[U], rr[U], rw[U];
+    // U vectors per tensor per iteration (k-th at offset k * kstep), all loads
+    // issued before any is consumed
+    auto batch = [&](int64_t v, int64_t kstep) {
+        uint32_t bm[U][N], bl[U][N], br[U][N];
+        uint4 rl[U], rr[U], rw[U];
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int64_t u = v + k * stride;
-                load_bytes<T>(pm + u * N, bm[k]);
-                load_bytes<T>(pl + u * N, bl[k]);
-                load_bytes<T>(pr + u * N, br[k]);
-                rl[k] = reinterpret_cast<const uint4*>(l)[u];
-                rr[k] = reinterpret_cast<const uint4*>(r)[u];
-                rw[k] = reinterpret_cast<const uint4*>(w)[u];
+        for (int k = 0; k < U; ++k) {
+            const int64_t u = v + k * kstep;
+            load_bytes<T>(pm + u * N, bm[k]);
+            load_bytes<T>(pl + u * N, bl[k]);
+            load_bytes<T>(pr + u * N, br[k]);
+            rl[k] = load16<NTL>(l4 + u);
+            rr[k] = load16<NTL>(r4 + u);
+            rw[k] = load16<NTL>(w4 + u);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) body(v + k * kstep, bm[k], bl[k], br[k], rl[k], rr[k], rw[k]);
+    };
+    if constexpr (CONTIG) {
+        const int64_t tile = (int64_t)U * kBlock;
+        const int64_t vb = e0 / N, nv = v1 - vb;
+        const int64_t per = ((nv + gridDim.x - 1) / gridDim.x + tile - 1) / tile * tile;
+        const int64_t lo = vb + (int64_t)blockIdx.x * per;
+        const int64_t hi = lo + per < v1 ? lo + per : v1;
+        int64_t base = lo;
+        for (; base + tile <= hi; base += tile) batch(base + threadIdx.x, kBlock);
+        for (int64_t u = base + threadIdx.x; u < hi; u += kBlock) one(u);
+    } else {
+        for (int64_t v = e0 / N + (int64_t)blockIdx.x * kBlock + threadIdx.x; v < v1; v += stride * U) {
+            if (v + (U - 1) * stride < v1) {
+                batch(v, stride);
+            } else {
+                for (int64_t u = v; u < v1; u += stride) one(u);
             }
-#pragma unroll
-            for (int k = 0; k < U; ++k) body(v + k * stride, bm[k], bl[k], br[k], rl[k], rr[k], rw[k]);
-        } else {
-            for (int64_t u = v; u < v1; u += stride) one(u);
         }
     }
     if (e1 == n && blockIdx.x == 0 && threadIdx.x < n - nvec * N) {
@@ -242,11 +301,30 @@ static int apply_impl(const uint8_t* mine, const uint8_t* from_left, const uint8
     for (const uint8_t* p : {mine, from_left, from_right})
         if ((uintptr_t)(p + 32) % N) return BAGUA_ERR_UNSUPPORTED;
     int64_t blocks = ((int64_t)(e1 - e0) / N + kBlock - 1) / kBlock;
-    if (blocks > 2 * kTargetBlocks) blocks = 2 * kTargetBlocks;
+    const ApplyCfg& c = kApplyCfg[apply_cfg()];
+    if (blocks > c.max_blocks) blocks = c.max_blocks;
     if (blocks < 1) blocks = 1;
-    launch(ring_apply_kernel<T, kApplyUnroll>, dim3(blocks), dim3(kBlock), 0, s, mine, from_left, from_right,
-           static_cast<S*>(t), static_cast<S*>(w), static_cast<S*>(l), static_cast<S*>(r), (int64_t)n, (int64_t)e0,
-           (int64_t)e1);
+    switch (apply_cfg()) {
+#define BAGUA_APPLY_LAUNCH(I)                                                                                      \
+    case I:                                                                                                        \
+        launch(ring_apply_kernel<T, kApplyCfg[I].u, kApplyCfg[I].sp, kApplyCfg[I].ntl, kApplyCfg[I].contig>,       \
+               dim3(blocks), dim3(kBlock), 0, s, mine, from_left, from_right, static_cast<S*>(t), static_cast<S*>(w), \
+               static_cast<S*>(l), static_cast<S*>(r), (int64_t)n, (int64_t)e0, (int64_t)e1);                      \
+        break;
+        BAGUA_APPLY_LAUNCH(0)
+        BAGUA_APPLY_LAUNCH(1)
+        BAGUA_APPLY_LAUNCH(2)
+        BAGUA_APPLY_LAUNCH(3)
+        BAGUA_APPLY_LAUNCH(4)
+        BAGUA_APPLY_LAUNCH(5)
+        BAGUA_APPLY_LAUNCH(6)
+        BAGUA_APPLY_LAUNCH(7)
+        BAGUA_APPLY_LAUNCH(8)
+        BAGUA_APPLY_LAUNCH(9)
+#undef BAGUA_APPLY_LAUNCH
+        default:
+            return BAGUA_ERR_UNSUPPORTED;
+    }
     return check_launch();
 }
 

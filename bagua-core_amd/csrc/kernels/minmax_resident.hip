@@ -63,7 +63,8 @@ constexpr int kResSlots = 64;
 
 struct ResidentSlot {
     uint64_t ticket;                 // monotonic ticket counter (one per workgroup at its start)
-    uint64_t pad0[7];
+    uint64_t gave_up;                // workgroups that timed out in the exchange (bagua_minmax_u8_resident_give_ups)
+    uint64_t pad0[6];
     uint64_t drained;                // workgroups done with the slot (one per workgroup after the exchange)
     uint64_t pad1[7];
     uint64_t gran[2 * kResMaxGrid];  // {tag << 32 | min key}, {tag << 32 | max key} per workgroup
@@ -379,6 +380,7 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
     __syncthreads();
     if (scratch[2 * W + 1] == 0u) {
         // gave up waiting: the whole workgroup folds the missing slices itself
+        if (t == 0) __hip_atomic_fetch_add(&a.slot->gave_up, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t l = 0xffffffffu, h = 0xffffffffu;
         fold_missing_slices<T, BLOCK>(a, s.cl, tag, l, h);
         l = wave_umin(l);
@@ -828,6 +830,27 @@ int release_stream_slot(hipStream_t s) {
     return rc;
 }
 
+// workgroups of stream `s`'s one-launch encodes that gave up waiting for their
+// chunk's partials (measurement: contention with other streams' kernels).
+// Synchronises `s`; *count = 0 when the stream never ran the one-launch encode.
+int resident_give_ups(hipStream_t s, uint64_t* count) {
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    *count = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || !g_res_dev[dev].ok) return BAGUA_OK;
+    ResidentDevice& d = g_res_dev[dev];
+    auto it = d.stream_slot.find(stream_key(s));
+    if (it == d.stream_slot.end()) return BAGUA_OK;
+    if (hipMemcpyAsync(d.probe_host, &d.slots[it->second].gave_up, sizeof(uint64_t), hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+        g_last_hip_error = (int)hipGetLastError();
+        return BAGUA_ERR_HIP;
+    }
+    *count = *d.probe_host;
+    return BAGUA_OK;
+}
+
 int resident_slots_in_use(int dev) {
     std::lock_guard<std::mutex> lk(g_res_mu);
     if (dev < 0 || dev >= 64 || !g_res_dev[dev].ok) return 0;
@@ -851,6 +874,11 @@ extern "C" int bagua_minmax_u8_release_stream(bagua_stream_t stream) {
 }
 
 extern "C" int bagua_minmax_u8_resident_slots_in_use(int device_id) { return bagua::resident_slots_in_use(device_id); }
+
+extern "C" int bagua_minmax_u8_resident_give_ups(bagua_stream_t stream, uint64_t* count) {
+    if (!count) return BAGUA_ERR_INVALID_ARG;
+    return bagua::resident_give_ups(static_cast<hipStream_t>(stream), count);
+}
 
 extern "C" int bagua_minmax_u8_resident_trace(void* device_buffer) {
     std::lock_guard<std::mutex> lk(bagua::g_res_mu);

@@ -96,6 +96,10 @@ int bagua_minmax_u8_resident_trace(void* device_buffer);
 int bagua_minmax_u8_release_stream(bagua_stream_t stream);
 /* Streams currently holding a slot on `device_id` (tests and diagnostics). */
 int bagua_minmax_u8_resident_slots_in_use(int device_id);
+/* measurement: how many workgroups of `stream`'s one-launch encodes timed out waiting
+ * for their chunk's partials (contention with other streams' kernels) and re-read the
+ * missing slices instead.  Synchronises `stream`. */
+int bagua_minmax_u8_resident_give_ups(bagua_stream_t stream, uint64_t* count);
 /* decompress_uint8_to_{f32,f16}_host (K:667-681) */
 int bagua_minmax_u8_decompress(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
                                int num_chunks, void* output, bagua_stream_t stream);

@@ -25,7 +25,8 @@ from collections import defaultdict
 
 KERNELS = ("minmax_resident_encode_kernel",
            "minmax_partials_kernel", "minmax_quantize_kernel", "minmax_dequantize_kernel",
-           "onebit_encode_kernel", "onebit_decode_kernel", "dequant_reduce_kernel")
+           "onebit_encode_kernel", "onebit_decode_kernel", "dequant_reduce_kernel",
+           "ring_mix_kernel", "ring_apply_kernel")
 
 
 def short(name: str) -> str | None:
