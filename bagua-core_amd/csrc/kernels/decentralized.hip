@@ -48,9 +48,22 @@ constexpr ApplyCfg kApplyCfg[] = {
     {4, 0x0, true, false, 4096},   // 7: nt loads, default stores
     {4, 0xF, false, true, 1024},   // 8: contiguous, 4 workgroups per CU
     {4, 0xF, false, false, 1024},  // 9: grid-strided, 1024 workgroups
+    {4, 0xF, true, true, 4096},    // 10: contiguous + nt loads
+    {2, 0xF, false, true, 4096},   // 11: contiguous, U = 2
+    {4, 0xF, false, true, 2048},   // 12: contiguous, 2048 workgroups
+    {4, 0xF, false, true, 8192},   // 13: contiguous, 8192 workgroups
+    {2, 0xF, true, true, 8192},    // 14: contiguous, U = 2, nt loads, 8192 workgroups
+    {8, 0xF, false, true, 4096},   // 15: contiguous, U = 8
+    {2, 0xF, true, true, 16384},   // 16
+    {2, 0xF, true, true, 32768},   // 17: one tile per workgroup
+    {4, 0xF, true, true, 8192},    // 18
+    {1, 0xF, true, true, 16384},   // 19
+    {1, 0xF, true, true, 65536},   // 20: one tile per workgroup
+    {2, 0xF, true, false, 8192},   // 21: grid-strided, U = 2, nt loads
+    {2, 0xC, true, true, 8192},    // 22: as 14 with default-policy l / r stores
 };
 constexpr int kApplyNumCfg = (int)(sizeof(kApplyCfg) / sizeof(kApplyCfg[0]));
-constexpr int kApplyDefaultCfg = 0;
+constexpr int kApplyDefaultCfg = 20;  // one 256-vector tile per workgroup, nt loads (profiles/r03_ring_apply_sweep3.jsonl)
 static int apply_cfg() {
     const char* e = getenv("BAGUA_RING_APPLY_CFG");
     const int c = (e && *e) ? atoi(e) : kApplyDefaultCfg;
@@ -74,7 +87,7 @@ __device__ __forceinline__ float mix(float t, float l, float r, float w, float f
     return addmul<T>(t, w, f53);
 }
 
-template <typename T, int U>
+template <typename T, int U, bool CONTIG = false>
 __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* __restrict__ t,
                                                           const typename T::storage* __restrict__ l,
                                                           const typename T::storage* __restrict__ r,
@@ -109,21 +122,35 @@ __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* _
     // issued before any is consumed; the last partial iteration goes one by one.
     // All four streams load non-temporally: default-policy t/w loads (or l/r) were
     // slower (profiles/r01_ring_mix_policy_ab.jsonl)
-    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nvec; v += stride * U) {
-        if (v + (U - 1) * stride < nvec) {
-            uint4 rt[U], rl[U], rr[U], rw[U];
+    auto batch = [&](int64_t v, int64_t kstep) {
+        uint4 rt[U], rl[U], rr[U], rw[U];
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                rt[k] = nt_load16(t4 + v + k * stride);
-                rl[k] = nt_load16(l4 + v + k * stride);
-                rr[k] = nt_load16(r4 + v + k * stride);
-                rw[k] = nt_load16(w4 + v + k * stride);
+        for (int k = 0; k < U; ++k) {
+            rt[k] = nt_load16(t4 + v + k * kstep);
+            rl[k] = nt_load16(l4 + v + k * kstep);
+            rr[k] = nt_load16(r4 + v + k * kstep);
+            rw[k] = nt_load16(w4 + v + k * kstep);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) body(v + k * kstep, rt[k], rl[k], rr[k], rw[k]);
+    };
+    if constexpr (CONTIG) {  // one contiguous range per workgroup
+        const int64_t tile = (int64_t)U * kBlock;
+        const int64_t per = ((nvec + gridDim.x - 1) / gridDim.x + tile - 1) / tile * tile;
+        const int64_t lo = (int64_t)blockIdx.x * per;
+        const int64_t hi = lo + per < nvec ? lo + per : nvec;
+        int64_t base = lo;
+        for (; base + tile <= hi; base += tile) batch(base + threadIdx.x, kBlock);
+        for (int64_t u = base + threadIdx.x; u < hi; u += kBlock)
+            body(u, nt_load16(t4 + u), nt_load16(l4 + u), nt_load16(r4 + u), nt_load16(w4 + u));
+    } else {
+        for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nvec; v += stride * U) {
+            if (v + (U - 1) * stride < nvec) {
+                batch(v, stride);
+            } else {
+                for (int64_t u = v; u < nvec; u += stride)
+                    body(u, nt_load16(t4 + u), nt_load16(l4 + u), nt_load16(r4 + u), nt_load16(w4 + u));
             }
-#pragma unroll
-            for (int k = 0; k < U; ++k) body(v + k * stride, rt[k], rl[k], rr[k], rw[k]);
-        } else {
-            for (int64_t u = v; u < nvec; u += stride)
-                body(u, nt_load16(t4 + u), nt_load16(l4 + u), nt_load16(r4 + u), nt_load16(w4 + u));
         }
     }
     if (blockIdx.x == 0 && threadIdx.x < n - nvec * N) {  // ragged tail
@@ -281,9 +308,15 @@ static int mix_impl(void* t, const void* l, const void* r, const void* w, int n,
     if (!aligned16(t) || !aligned16(l) || !aligned16(r) || !aligned16(w)) return BAGUA_ERR_UNSUPPORTED;
     const int nblk = ws ? minmax_partials_blocks(n, Vec<T>::N, 1, ws_bytes) : 0;
     if (nblk < 1) return BAGUA_ERR_WORKSPACE;
-    launch(ring_mix_kernel<T, kMixUnroll>, dim3(nblk), dim3(kBlock), 0, s, static_cast<S*>(t),
-                       static_cast<const S*>(l), static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13,
-                       f53, static_cast<uint2*>(ws));
+    const char* e = getenv("BAGUA_RING_MIX_CONTIG");  // A/B (tools/ring_apply_sweep.py)
+    if (e && e[0] == '1')
+        launch(ring_mix_kernel<T, kMixUnroll, true>, dim3(nblk), dim3(kBlock), 0, s, static_cast<S*>(t),
+               static_cast<const S*>(l), static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13, f53,
+               static_cast<uint2*>(ws));
+    else
+        launch(ring_mix_kernel<T, kMixUnroll>, dim3(nblk), dim3(kBlock), 0, s, static_cast<S*>(t),
+               static_cast<const S*>(l), static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13, f53,
+               static_cast<uint2*>(ws));
     return check_launch();
 }
 
@@ -321,6 +354,19 @@ static int apply_impl(const uint8_t* mine, const uint8_t* from_left, const uint8
         BAGUA_APPLY_LAUNCH(7)
         BAGUA_APPLY_LAUNCH(8)
         BAGUA_APPLY_LAUNCH(9)
+        BAGUA_APPLY_LAUNCH(10)
+        BAGUA_APPLY_LAUNCH(11)
+        BAGUA_APPLY_LAUNCH(12)
+        BAGUA_APPLY_LAUNCH(13)
+        BAGUA_APPLY_LAUNCH(14)
+        BAGUA_APPLY_LAUNCH(15)
+        BAGUA_APPLY_LAUNCH(16)
+        BAGUA_APPLY_LAUNCH(17)
+        BAGUA_APPLY_LAUNCH(18)
+        BAGUA_APPLY_LAUNCH(19)
+        BAGUA_APPLY_LAUNCH(20)
+        BAGUA_APPLY_LAUNCH(21)
+        BAGUA_APPLY_LAUNCH(22)
 #undef BAGUA_APPLY_LAUNCH
         default:
             return BAGUA_ERR_UNSUPPORTED;

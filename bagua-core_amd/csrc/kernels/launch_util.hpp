@@ -33,6 +33,13 @@ inline void launch(F kernel, const dim3& grid, const dim3& block, uint32_t shmem
     hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, t.start, t.stop, 0u, args...);
 }
 
+// launch-shape knob read per call (measurement sweeps, tools/grid_sweep.py);
+// `dflt` when unset
+inline int tune_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return (e && *e) ? atoi(e) : dflt;
+}
+
 inline int check_launch() {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -28,12 +28,14 @@ namespace bagua {
 constexpr int kVecPerBlockTile = kBlock * kSubtiles;  // 1024 x 16-B vectors = 16 KiB in flight per block
 // Launch shapes picked on MI355X with tools/stream_probe.hip:
 // the read-only min/max pass wants 8 vectors in flight per lane on 4 blocks
-// per CU; quantise 4 per lane on 8 blocks per CU; dequantise 4 per lane on
-// 16 blocks per CU (grid-strided).
+// per CU; quantise and dequantise 4 per lane.  Round 3 (tools/grid_sweep.py,
+// profiles/r03_grid_sweep.jsonl): more, shorter workgroups let the dispatcher
+// balance the tail -- dequantise one tile per workgroup (16384 for 256 MiB f32:
+// 48.25 -> 47.75 us), quantise 32 per CU (51.0 -> 50.1 us).
 constexpr int kPartialsSub = 8;
 constexpr int kPartialsBlocks = 1024;
-constexpr int kQuantBlocks = 2048;
-constexpr int kDequantBlocks = 4096;
+constexpr int kQuantBlocks = 8192;
+constexpr int kDequantBlocks = 16384;
 
 __device__ __forceinline__ int64_t chunk_valid(int64_t in_num_elem, int64_t cs, int c) {
     // K:538-545: remaining elements, clamped to [0, chunk_size]
@@ -348,7 +350,9 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
         launch(minmax_partials_kernel<T>, dim3(nblk, nact), dim3(kBlock), 0, s,
                            static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, partials);
     if (stages & 2)
-        launch((minmax_quantize_kernel<T, true>), dim3(blocks_for(e1 - e0, Vec<T>::N, nact), nact),
+        launch((minmax_quantize_kernel<T, true>),
+               dim3(blocks_for(e1 - e0, Vec<T>::N, nact, kSubtiles, tune_int("BAGUA_TUNE_QUANT_BLOCKS", kQuantBlocks)),
+                    nact),
                            dim3(kBlock), 0, s, static_cast<const S*>(input), (int64_t)in_num_elem,
                            (int64_t)cs, (int64_t)e0, (int64_t)e1, target, partials, nblk, out, chunk_offset,
                            (int64_t)out_bytes, p);
@@ -469,7 +473,8 @@ static int decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p, vo
     // nt stores: with default-policy stores the decoded bucket's dirty lines sit in the
     // Infinity Cache and the next encode's pass 2 pays for them (85 -> 119 us per
     // 256 MiB encode)
-    launch(minmax_dequantize_kernel<T, true>, dim3(blocks_for(e1 - e0, Vec<T>::N, p, kSubtiles, kDequantBlocks), p),
+    launch(minmax_dequantize_kernel<T, true>,
+           dim3(blocks_for(e1 - e0, Vec<T>::N, p, kSubtiles, tune_int("BAGUA_TUNE_DEQUANT_BLOCKS", kDequantBlocks)), p),
            dim3(kBlock), 0, s, in, chunk_offset, (int64_t)cs, (int64_t)e0, (int64_t)e1, static_cast<S*>(out));
     return check_launch();
 }

@@ -26,11 +26,14 @@ namespace bagua {
 constexpr int kObTile = 1024;
 constexpr int kObTileBytes = 128;
 constexpr int kObFinalizeThreads = 1024;
-// encode grid cap: 1024 workgroups (4 per CU) with 64 B of loads in flight per
-// lane (one tile per iteration for 32-bit types, two for 16-bit ones) beat
-// 2048 workgroups and 2 tiles by 3 % (f32) to 5 % (bf16) on the 256 MiB step
-// (profiles/r01_onebit_shape_sweep.jsonl)
-constexpr int kObEncodeBlocks = 1024;
+// encode / decode grid caps: 64 B of loads in flight per lane (one tile per
+// iteration for 32-bit types, two for 16-bit ones).  Round 1 picked 1024 encode
+// workgroups over 2048 (profiles/r01_onebit_shape_sweep.jsonl); round 3 found
+// one tile per wave better still (16384 workgroups for 2^26 f32 elements):
+// encode 45.8 -> 43.8 us, decode 42.7 -> 42.0 us per 256 MiB
+// (tools/grid_sweep.py, profiles/r03_grid_sweep.jsonl)
+constexpr int kObEncodeBlocks = 16384;
+constexpr int kObDecodeBlocks = 16384;
 
 __device__ __forceinline__ int64_t ob_valid(int64_t in_num_elem, int64_t cs, int c) {
     int64_t r = in_num_elem - (int64_t)c * cs;
@@ -590,7 +593,8 @@ static int ob_compress_impl(const void* input, int in_num_elem, int cs, int p, u
     // 77 us instead of 47 (profiles/r01_decode_store_ab.jsonl)
     if (stage != 2 && te > tb)
         launch(onebit_encode_kernel<T, sizeof(S) == 4 ? 1 : 2, true>,
-               dim3(ob_blocks(te - tb, nact, kObEncodeBlocks), nact), dim3(kBlock), 0, s,
+               dim3(ob_blocks(te - tb, nact, tune_int("BAGUA_TUNE_OB_ENCODE_BLOCKS", kObEncodeBlocks)), nact),
+               dim3(kBlock), 0, s,
                static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, out, co, partials, tiles, tb,
                te);
     if (stage != 1)
@@ -612,7 +616,9 @@ static int ob_decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p,
     if (te <= t_begin) return BAGUA_OK;
     // default-policy stores: 43 us vs 50 us with nt stores per 256 MiB decode, and the
     // next encode (nt loads) is unaffected (profiles/r01_decode_store_ab.jsonl)
-    launch(onebit_decode_kernel<T, false>, dim3(ob_blocks(te - t_begin, p), p), dim3(kBlock), 0, s, in, co,
+    launch(onebit_decode_kernel<T, false>,
+           dim3(ob_blocks(te - t_begin, p, tune_int("BAGUA_TUNE_OB_DECODE_BLOCKS", kObDecodeBlocks)), p), dim3(kBlock), 0,
+           s, in, co,
            (int64_t)cs, static_cast<S*>(out), t_begin, te);
     return check_launch();
 }

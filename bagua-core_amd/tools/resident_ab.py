@@ -127,9 +127,9 @@ def main():
         wall = (time.perf_counter() - t0) / steps * 1e6
         if not events:
             return wall, None, None
-        enc = [r[0].elapsed_time(r[1]) * 1e3 for r in ev]
-        dec = [r[2].elapsed_time(r[3]) * 1e3 for r in ev]
-        return wall, enc, dec
+        te = [r[0].elapsed_time(r[1]) * 1e3 for r in ev]
+        td = [r[2].elapsed_time(r[3]) * 1e3 for r in ev]
+        return wall, te, td
 
     allenc = {nm: [] for nm, _, _ in libs}
     alldec = {nm: [] for nm, _, _ in libs}
@@ -139,12 +139,12 @@ def main():
         for name, L, gu in order:
             run(L, 5, False)
             wall, _, _ = run(L, a.steps, False)
-            _, enc, dec = run(L, a.steps, True)
-            allenc[name] += enc
-            alldec[name] += dec
+            _, te, td = run(L, a.steps, True)
+            allenc[name] += te
+            alldec[name] += td
             allwall[name].append(wall)
-            print(json.dumps({"round": r, "build": name, "step_wall_us": round(wall, 2), "encode_us": stats(enc),
-                              "decode_us": stats(dec)}), flush=True)
+            print(json.dumps({"round": r, "build": name, "step_wall_us": round(wall, 2), "encode_us": stats(te),
+                              "decode_us": stats(td)}), flush=True)
     for name, L, gu in libs:
         out = {"build": name, "summary": True, "encode_us": stats(allenc[name]), "decode_us": stats(alldec[name]),
                "step_wall_us": stats(allwall[name])}

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--elements", type=int, default=1 << 27)
+    ap.add_argument("--mix", action="store_true", help="also A/B the mix pass (BAGUA_RING_MIX_CONTIG)")
     a = ap.parse_args()
     n = a.elements
     cfgs = [int(c) for c in a.cfgs.split(",")]
@@ -122,6 +123,54 @@ def main():
                           "op_ms_mean": round(float(np.mean(res[c]["op_ms"])), 4),
                           "identical_outputs": True}), flush=True)
     os.environ.pop("BAGUA_RING_APPLY_CFG", None)
+    if a.mix:
+        mix_ab(a, n, tens, init, comp["mine"], S, ws, wsb, stream, sp)
+
+
+def mix_ab(a, n, tens, init, out, S, ws, wsb, stream, sp):
+    """ring_mix_kernel grid-strided vs contiguous ranges (BAGUA_RING_MIX_CONTIG):
+    identical mixed tensor and identical quantised bytes (the quantise pass folds
+    the mix's min/max partials), then the mix alone timed, interleaved."""
+    def mix():
+        return K.bagua_ring_mix_minmax(BF16, tens["t"].data_ptr(), tens["l"].data_ptr(), tens["r"].data_ptr(),
+                                       tens["w"].data_ptr(), n, ws.data_ptr(), wsb, sp)
+
+    ref = None
+    for c in ("0", "1"):
+        os.environ["BAGUA_RING_MIX_CONTIG"] = c
+        for k in tens:
+            tens[k].copy_(init[k])
+        torch.cuda.synchronize()
+        N.check(mix(), "mix")
+        N.check(K.bagua_minmax_u8_compress_stage(2, BF16, tens["t"].data_ptr(), n, n, 1, out.data_ptr(), S,
+                                                 ws.data_ptr(), wsb, -1, sp), "quantise")
+        torch.cuda.synchronize()
+        got = (tens["t"].view(torch.int16).cpu(), out.cpu())
+        if ref is None:
+            ref = got
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), "mix variants differ"
+    res = {"0": [], "1": []}
+    for rnd in range(a.rounds):
+        for c in (("0", "1") if rnd % 2 == 0 else ("1", "0")):
+            os.environ["BAGUA_RING_MIX_CONTIG"] = c
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+            for e0, e1 in ev:
+                e0.record(stream)
+                e1.record(stream)
+            for _ in range(3):
+                mix()
+            for e0, e1 in ev:
+                K.bagua_time_next_kernel(e0.cuda_event, e1.cuda_event)
+                mix()
+            torch.cuda.synchronize()
+            res[c].append(float(np.mean([e0.elapsed_time(e1) * 1e3 for e0, e1 in ev])))
+    for c in ("0", "1"):
+        us = float(np.mean(res[c]))
+        print(json.dumps({"mix_contig": c == "1", "summary": True, "mix_us_mean": round(us, 2),
+                          "mix_tbs": round(10 * n / (us * 1e-6) / 1e12, 3),
+                          "mix_frac_of_8tbs": round(10 * n / (us * 1e-6) / 8e12, 4), "identical_outputs": True}),
+              flush=True)
+    os.environ.pop("BAGUA_RING_MIX_CONTIG", None)
 
 
 if __name__ == "__main__":
