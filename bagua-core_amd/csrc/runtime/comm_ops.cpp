@@ -125,14 +125,20 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
     const bagua_tensor_t rv = u8_view(recv.ptr(), k.S, c->device_id);
     // 1. compress every chunk (target -1)
     TRY(bagua_tensor_compress_into(t, method, k.p, s, -1, &sv));
-    // 2. alltoall: slot j of recv <- rank j's segment `rank` (one rank: the same bytes by a
-    // device copy instead of RCCL's single-rank copy kernel; 1 GiB op 1.257 -> 1.222 ms)
-    if (k.p == 1)
+    // 2. alltoall: slot j of recv <- rank j's segment `rank`.  One rank receives its own
+    // bytes: the MinMax steps below read them from `send` itself (their reads and the
+    // requantise's writes are separate kernels in stream order), the 1-bit middle step
+    // -- one kernel that reads every segment's header while rewriting its own -- from a
+    // device copy (RCCL's single-rank copy kernel was slower: 1 GiB op 1.257 -> 1.222 ms)
+    const bool self_alias = k.p == 1 && method == BAGUA_COMPRESSION_MINMAX_UINT8;
+    if (k.p == 1 && !self_alias)
         TRY(hipMemcpyAsync(recv.as<void>(), send.as<void>(), k.S, hipMemcpyDeviceToDevice, c->stream) == hipSuccess
                 ? BAGUA_OK
                 : BAGUA_ERR_HIP);
-    else
+    else if (k.p > 1)
         TRY(c->t->alltoall(send.as<void>(), recv.as<void>(), k.S / k.p, BAGUA_DTYPE_U8, c->stream));
+    uint8_t* const rbuf = self_alias ? send.as<uint8_t>() : recv.as<uint8_t>();
+    const bagua_tensor_t* const rview = self_alias ? &sv : &rv;
     // 3. reduce the p received versions of the own chunk and requantise it into send[rank]
     bool done = false;
     // the fused kernels treat every allocated element as valid (the reference
@@ -141,7 +147,7 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
         const size_t ws_bytes = bagua_minmax_u8_workspace_bytes((int)k.cs, k.p);
         const uint64_t ws = stream_workspace(c->device_id, s, ws_bytes);
         if (!ws) return finish(c, BAGUA_ERR_OOM);
-        rc = bagua_minmax_u8_reduce_requantize(t->dtype, recv.as<uint8_t>(), k.S, (int)k.cs, k.p,
+        rc = bagua_minmax_u8_reduce_requantize(t->dtype, rbuf, k.S, (int)k.cs, k.p,
                                                (void*)(uintptr_t)t->ptr, average, send.as<uint8_t>(), k.S, k.rank,
                                                (void*)(uintptr_t)ws, ws_bytes, (void*)(uintptr_t)s);
         if (rc == BAGUA_OK) done = true;
@@ -158,7 +164,7 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
         else if (rc != BAGUA_ERR_UNSUPPORTED) return finish(c, rc);
     }
     if (!done) {
-        TRY(bagua_tensor_decompress_from(t, method, k.p, &rv, s));
+        TRY(bagua_tensor_decompress_from(t, method, k.p, rview, s));
         TRY(bagua_tensor_reduce_inplace(t, k.p, k.rank, average, s));
         TRY(bagua_tensor_compress_into(t, method, k.p, s, k.rank, &sv));
     }
@@ -704,26 +710,32 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
         // :61-64 whole-bucket compress (n_chunks = 1)
         TRY(bagua_tensor_compress_into(t, method, 1, s, -1, &mv));
     }
-    // :98-115 ring exchange inside one group
+    // :98-115 ring exchange inside one group.  One rank is its own left and right
+    // peer: what it would receive are its own bytes, so the op reads `mine` in their
+    // place (RCCL's self send/recv of 2 x S bytes took 206 us for 2^27 bf16).
     const int p = (int)c->nranks, r = (int)c->rank;
     const int lpeer = (r + p - 1) % p, rpeer = (r + 1) % p;
-    TRY(c->t->group_start());
-    rc = bagua_comm_send(c, &mv, lpeer);
-    if (!rc) rc = bagua_comm_send(c, &mv, rpeer);
-    if (!rc) rc = bagua_comm_recv(c, &lv, lpeer);
-    if (!rc) rc = bagua_comm_recv(c, &rv, rpeer);
-    const int rc_end = c->t->group_end();
-    if (rc || rc_end) return finish(c, rc ? rc : rc_end);
+    if (p > 1) {
+        TRY(c->t->group_start());
+        rc = bagua_comm_send(c, &mv, lpeer);
+        if (!rc) rc = bagua_comm_send(c, &mv, rpeer);
+        if (!rc) rc = bagua_comm_recv(c, &lv, lpeer);
+        if (!rc) rc = bagua_comm_recv(c, &rv, rpeer);
+        const int rc_end = c->t->group_end();
+        if (rc || rc_end) return finish(c, rc ? rc : rc_end);
+    }
+    const bagua_tensor_t* from_l = p > 1 ? &lv : &mv;
+    const bagua_tensor_t* from_r = p > 1 ? &rv : &mv;
     // :126-151
     if (fused) {
-        rc = bagua_ring_apply_minmax(t->dtype, mine.as<uint8_t>(), lbuf.as<uint8_t>(), rbuf.as<uint8_t>(), S, n, tp,
-                                     wp, lp, rp, sp);
+        rc = bagua_ring_apply_minmax(t->dtype, mine.as<uint8_t>(), (const uint8_t*)(uintptr_t)from_l->ptr,
+                                     (const uint8_t*)(uintptr_t)from_r->ptr, S, n, tp, wp, lp, rp, sp);
         if (rc == BAGUA_OK) return finish(c, BAGUA_OK);
         if (rc != BAGUA_ERR_UNSUPPORTED) return finish(c, rc);
     }
-    TRY(bagua_tensor_decompress_from(t, method, 1, &lv, s));
+    TRY(bagua_tensor_decompress_from(t, method, 1, from_l, s));
     TRY(bagua_tensor_add_inplace(left, t, s));
-    TRY(bagua_tensor_decompress_from(t, method, 1, &rv, s));
+    TRY(bagua_tensor_decompress_from(t, method, 1, from_r, s));
     TRY(bagua_tensor_add_inplace(right, t, s));
     TRY(bagua_tensor_decompress_from(t, method, 1, &mv, s));
     TRY(bagua_tensor_add_inplace(t, weight, s));
