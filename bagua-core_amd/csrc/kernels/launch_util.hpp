@@ -30,6 +30,9 @@ template <typename F, typename... Args>
 inline void launch(F kernel, const dim3& grid, const dim3& block, uint32_t shmem, hipStream_t s, Args... args) {
     const KernelTiming t = g_kernel_timing;
     g_kernel_timing = KernelTiming{};
+    // one launch path for timed and untimed launches: hipLaunchKernel instead of the
+    // Ext call when nothing is timed costs the host the same (4.6-5.2 us per launch
+    // either way, profiles/r03_host_overhead_ab.jsonl)
     hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, t.start, t.stop, 0u, args...);
 }
 

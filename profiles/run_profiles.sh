@@ -21,9 +21,9 @@ step() {  # name timeout cmd...: stop at the first failure (fault, abort, time l
 }
 B=(bench.py --steps 30 --warmup 5 --no-cpu-baseline)
 step trace_codec 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o codec -- \
-  python3 "${B[@]}" > "$OUT/codec_under_rocprof.json"
+  python3 "${B[@]}" --no-cold > "$OUT/codec_under_rocprof.json"
 step trace_onebit 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_ob" -o onebit -- \
-  python3 "${B[@]}" --workload onebit > "$OUT/onebit_under_rocprof.json"
+  python3 "${B[@]}" --no-cold --workload onebit > "$OUT/onebit_under_rocprof.json"
 step fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
   python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-cold
 step write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
