@@ -65,10 +65,11 @@ class BaguaCommBackendPy:
         if name not in self._names:
             raise RuntimeError(f"TensorError: tensor {name} is not registered in any bucket")
         # the tensor's current storage goes with it (the reference reads data_ptr at run time)
-        raw = tensor.raw()
-        N.check(N.C.bagua_comm_backend_mark_communication_ready_desc(self._handle, name.encode(),
-                                                                    int(ready_cuda_event_ptr or 0), ctypes.byref(raw)),
-                "mark_communication_ready")
+        rc = N.C.bagua_comm_backend_mark_communication_ready_desc(self._handle, name.encode(),
+                                                                 int(ready_cuda_event_ptr or 0),
+                                                                 ctypes.byref(tensor._current()))
+        if rc:
+            N.check(rc, "mark_communication_ready")
 
     def wait_pending_comm_ops(self) -> int:
         """lib.rs:321-337: wait for every scheduled op; returns how many finished."""

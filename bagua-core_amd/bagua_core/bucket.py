@@ -223,16 +223,14 @@ class BaguaBucketPy:
     # ---- readiness (datatypes/mod.rs:1256-1266, 793-813), by tensor name --------
     def mark_tensor_ready(self, tensor: BaguaTensorPy, ready_cuda_event_ptr: int = 0) -> None:
         # the tensor's CURRENT storage (data_ptr read at run time, datatypes/mod.rs:775-791)
-        raw = tensor.raw()
         N.check(N.C.bagua_bucket_mark_tensor_ready_desc(self._handle, tensor.name().encode(),
-                                                        int(ready_cuda_event_ptr), ctypes.byref(raw)),
+                                                        int(ready_cuda_event_ptr), ctypes.byref(tensor._current())),
                 f"tensor {tensor.name()} is not in bucket {self.name} (or changed dtype/device)")
 
     def _refresh(self) -> None:
         """re-read every tensor's storage (a .data / set_ swap after the bucket was built)"""
         for t in self._tensors:
-            raw = t.raw()
-            N.check(N.C.bagua_bucket_refresh_tensor(self._handle, t.name().encode(), ctypes.byref(raw)),
+            N.check(N.C.bagua_bucket_refresh_tensor(self._handle, t.name().encode(), ctypes.byref(t._current())),
                     f"tensor {t.name()} changed dtype or device")
 
     def ready_for_comm(self) -> bool:

@@ -60,6 +60,12 @@ class BaguaTensorPy:
         self._pool_ptr = 0
         self._raw = None
         self._streams: set[int] = set()
+        # cached descriptor of the torch-backed tensor (the device is fixed; pointer,
+        # size and dtype are re-read from the torch tensor on every use: a `.data` swap)
+        self._desc = N.bagua_tensor_t()
+        self._desc.dtype = spec[0]
+        self._desc.device_id = torch_tensor.device.index if torch_tensor.device.index is not None \
+            else torch.cuda.current_device()
 
     # ---- construction from a pool buffer (compress output) ------------------
     @classmethod
@@ -88,16 +94,27 @@ class BaguaTensorPy:
             self._pool_ptr = 0
 
     def raw(self) -> N.bagua_tensor_t:
+        """A fresh descriptor of the tensor's current storage."""
         if self._torch is None:
             return self._raw
         t = self._torch
-        r = N.bagua_tensor_t()
-        r.ptr = t.data_ptr()
-        r.num_elem = t.numel()
-        r.num_elem_allocated = t.numel()
-        r.dtype = _DTYPES[t.dtype][0]
-        r.device_id = t.device.index if t.device.index is not None else torch.cuda.current_device()
-        return r
+        n = t.numel()
+        return N.bagua_tensor_t(t.data_ptr(), n, n, _DTYPES[t.dtype][0], self._desc.device_id)
+
+    def _current(self) -> N.bagua_tensor_t:
+        """The cached descriptor refreshed in place from the torch tensor: the
+        scheduler's per-mark path allocates no ctypes object (the reference reads
+        data_ptr / numel at run time, datatypes/mod.rs:775-791)."""
+        if self._torch is None:
+            return self._raw
+        t = self._torch
+        d = self._desc
+        n = t.numel()
+        d.ptr = t.data_ptr()
+        d.num_elem = n
+        d.num_elem_allocated = n
+        d.dtype = _DTYPES[t.dtype][0]
+        return d
 
     # ---- accessors (lib.rs:280-298) -----------------------------------------
     def name(self) -> str:

@@ -18,6 +18,7 @@ int pool_trim(int device_id);
 int pool_alloc_block(int device_id, size_t bytes, uint64_t* out);  // no capture-arena bookkeeping
 int pool_free_block(uint64_t ptr);
 void* pool_capture_begin();
+void pool_reap(int device_id);
 int pool_capture_end(void* arena);
 int pool_capture_release(void* arena);
 size_t pool_bytes(int device_id, bool cached);
@@ -26,6 +27,7 @@ size_t pool_bytes_pending(int device_id);
 // Per-(device, stream) scratch reused by every launch on that stream; stream
 // order makes reuse safe without host synchronisation.
 uint64_t stream_workspace(int device_id, uint64_t stream, size_t bytes);
+uint64_t stream_workspace_generation();
 // Frees the stream's workspace after the stream has drained (communicator teardown).
 int release_stream_workspace(int device_id, uint64_t stream);
 size_t stream_workspace_count();

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -57,19 +58,32 @@ static std::map<WorkspaceKey, std::pair<uint64_t, size_t>>& workspaces() {
     return *cache;
 }
 
+static std::atomic<uint64_t> g_ws_generation{0};
+
+// bumped whenever a stream's workspace block is replaced or freed: a HIP graph that
+// baked a workspace address (the scheduler's bucket graphs) is rebuilt when it sees
+// a newer generation than the one it was captured with
+uint64_t stream_workspace_generation() { return g_ws_generation.load(); }
+
 uint64_t stream_workspace(int device_id, uint64_t stream, size_t bytes) {
     std::lock_guard<std::mutex> g(g_ws_mu);
     auto& slot = workspaces()[workspace_key(device_id, stream)];
     if (slot.second >= bytes && slot.first) return slot.first;
     if (slot.first) {
-        // growing: queued work on this stream may still read the old block
-        (void)hipStreamSynchronize((hipStream_t)(uintptr_t)stream);
+        // growing: queued work on this stream may still read the old block (under
+        // capture the sync fails and invalidates the capture: the caller runs eagerly)
+        if (hipStreamSynchronize((hipStream_t)(uintptr_t)stream) != hipSuccess) {
+            (void)hipGetLastError();
+            return 0;
+        }
         pool_free(slot.first);
         slot = {0, 0};
+        ++g_ws_generation;
     }
     uint64_t p = 0;
     const size_t want = bytes < 65536 ? 65536 : bytes;
-    if (pool_alloc(device_id, want, &p) != BAGUA_OK) return 0;
+    // a stream's workspace outlives any op, so it never belongs to a capture arena
+    if (pool_alloc_block(device_id, want, &p) != BAGUA_OK) return 0;
     slot = {p, want};
     return p;
 }
@@ -82,6 +96,7 @@ int release_stream_workspace(int device_id, uint64_t stream) {
     if (hipStreamSynchronize((hipStream_t)(uintptr_t)stream) != hipSuccess) return BAGUA_ERR_HIP;
     if (it->second.first) pool_free(it->second.first);
     workspaces().erase(it);
+    ++g_ws_generation;
     return BAGUA_OK;
 }
 

@@ -796,11 +796,15 @@ def bench_backend(args, world: int, rank: int, local_rank: int):
     backend.register_ordered_buckets(list(reversed(buckets)))
     events = [torch.cuda.Event() for _ in range(args.buckets)]
 
+    mark_s = []
+
     def iteration():
+        t0 = time.perf_counter()
         for b in reversed(range(args.buckets)):
             events[b].record()
             for t in tensors[b]:
                 backend.mark_communication_ready(t, events[b].cuda_event)
+        mark_s.append(time.perf_counter() - t0)
         done = backend.wait_pending_comm_ops()
         assert done == args.buckets, done
 
@@ -823,7 +827,10 @@ def bench_backend(args, world: int, rank: int, local_rank: int):
     cfg = {"workload": f"comm_backend_{args.buckets}x{args.bucket_mib}MiB_fp32_buckets_minmax_uint8",
            "bucket_elements": per, "buckets": args.buckets, "tensors_per_bucket": 4,
            "parallelism": f"dp{world}", "scheduler": type(backend).__module__ + "." + type(backend).__name__}
-    extra = {"per_bucket_us": round(ms * 1e3 / args.buckets, 2), "per_rank_gib_s": round(value / world, 2)}
+    extra = {"per_bucket_us": round(ms * 1e3 / args.buckets, 2), "per_rank_gib_s": round(value / world, 2),
+             # host time of the Python side per bucket (a ready event + one mark per tensor): the
+             # scheduler cannot run a bucket before its last tensor is marked
+             "mark_us_per_bucket": round(sorted(mark_s)[len(mark_s) // 2] * 1e6 / args.buckets, 2)}
     del backend, buckets, comm
     return value, ms, None, cfg, extra
 
