@@ -522,9 +522,10 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     torch.cuda.synchronize()
     raw = BaguaTensorPy(x, "gradient_bucket").raw()
 
-    def compressed_step(pieces=args.pieces):
+    def compressed_step(pieces=None):
         N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
-                                                              N.COMPRESSION_MINMAX_UINT8, pieces),
+                                                              N.COMPRESSION_MINMAX_UINT8,
+                                                              args.pieces if pieces is None else pieces),
                 "compressed allreduce")
 
     def fp32_step():
@@ -592,6 +593,8 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     # allgather) on a fresh communicator, recorded in headline_fallback.
     headline_fallback = None
     aborted = []
+    autotune = {}  # pieces -> s per step during the untimed choice (N > 1, --pieces 0)
+    user_pieces = args.pieces  # the other ops keep the library's own choice unless --pieces is given
 
     def expire_headline():
         aborted.append(True)
@@ -603,6 +606,13 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     try:
         if os.environ.get("BAGUA_BENCH_FAIL_HEADLINE"):  # test hook: exercise the fallback below
             comm.abort()
+        if world > 1 and args.pieces == 0:
+            # runtime piece-count choice for this node (part of the warmup, untimed): a few
+            # steps at each count, the fastest max-over-ranks time wins on every rank alike
+            for q in (1, 2, 4, 8):
+                autotune[str(q)] = timed(lambda q=q: compressed_step(q), 2, 1)
+            best = min(autotune, key=lambda q: autotune[q])
+            args.pieces = int(best)
         t_c = timed(compressed_step, args.steps, args.warmup)
         err = "timed out; communicator aborted" if aborted else None
     except Exception as e:  # noqa: BLE001 - an op error on every rank alike
@@ -642,7 +652,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     t_f = side("fp32_allreduce", fp32_step)
     # the same all-reduce with the 1-bit sign+scale codec (this repo's extension:
     # N/8 wire bytes per phase instead of N), fused middle step
-    def onebit_step(pieces=args.pieces):
+    def onebit_step(pieces=user_pieces):
         N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
                                                               N.COMPRESSION_ONEBIT, pieces), "1-bit allreduce")
 
@@ -671,7 +681,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             bufs = [(torch.randn(nb, device=dev, generator=g) * 1e-3).to(torch.bfloat16) for _ in range(4)]
             draws = [BaguaTensorPy(b, k).raw() for b, k in zip(bufs, "twlr")]
 
-            def dec_step(pieces=args.pieces):
+            def dec_step(pieces=user_pieces):
                 N.check(N.C.bagua_decentralized_low_precision_pipelined(
                     comm.handle, *[ctypes.byref(r) for r in draws], N.COMPRESSION_MINMAX_UINT8, pieces),
                     "decentralized")
@@ -744,7 +754,9 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
            "config_index": 4}
     extra = {"per_rank_gib_s": round(per_rank, 2), "fp32_allreduce_gib_s": round(fp32, 2),
              "ratio_vs_fp32": round(per_rank / fp32, 3), "fp32_ms_per_step": round(t_f * 1e3, 3),
-             "pieces": args.pieces or "auto", "unpieced_ms_per_step": round(t_u * 1e3, 3),
+             "pieces": args.pieces or "auto",
+             "pieces_autotune_ms_per_step": {q: round(v * 1e3, 3) for q, v in autotune.items()} or None,
+             "unpieced_ms_per_step": round(t_u * 1e3, 3),
              "pieces_sweep_ms_per_step": {q: round(v * 1e3, 3) for q, v in sweep.items()} or None,
              "comm_only_ms": round(t_comm * 1e3, 3),
              "comm_only_note": "RCCL alltoall + in-place allgather of the op's S compressed bytes, nothing else",
