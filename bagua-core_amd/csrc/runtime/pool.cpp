@@ -125,10 +125,6 @@ int pool_alloc_block(int device_id, size_t bytes, uint64_t* out) {
             return BAGUA_OK;
         }
     }
-    // no HIP allocation inside a capture (it would invalidate it): the capturing op
-    // fails cleanly instead and its caller runs it eagerly (the scheduler's bucket
-    // graphs) or warms the pool first
-    if (t_arena) return BAGUA_ERR_OOM;
     DeviceGuard guard(device_id);
     void* p = nullptr;
     hipError_t e = hipMalloc(&p, cls);
@@ -231,15 +227,6 @@ int pool_trim(int device_id) {
     (void)hipDeviceSynchronize();  // a cached block may still be read by queued work
     for (uint64_t p : release) (void)hipFree((void*)(uintptr_t)p);
     return BAGUA_OK;
-}
-
-// Moves every pending block of `device_id` whose streams have drained to the free
-// lists (non-blocking), e.g. before a capture, which must not allocate from HIP
-void pool_reap(int device_id) {
-    Pool& P = pool();
-    std::lock_guard<std::mutex> g(P.mu);
-    auto it = P.dev.find(device_id);
-    if (it != P.dev.end() && !it->second.pending.empty()) reap_pending(it->second, false);
 }
 
 void* pool_capture_begin() {

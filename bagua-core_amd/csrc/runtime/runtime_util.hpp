@@ -18,7 +18,6 @@ int pool_trim(int device_id);
 int pool_alloc_block(int device_id, size_t bytes, uint64_t* out);  // no capture-arena bookkeeping
 int pool_free_block(uint64_t ptr);
 void* pool_capture_begin();
-void pool_reap(int device_id);
 int pool_capture_end(void* arena);
 int pool_capture_release(void* arena);
 size_t pool_bytes(int device_id, bool cached);
