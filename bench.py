@@ -609,7 +609,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         if world > 1 and args.pieces == 0:
             # runtime piece-count choice for this node (part of the warmup, untimed): a few
             # steps at each count, the fastest max-over-ranks time wins on every rank alike
-            for q in (1, 2, 4, 8):
+            for q in (1, 2, 4, 8, 16):
                 autotune[str(q)] = timed(lambda q=q: compressed_step(q), 2, 1)
             best = min(autotune, key=lambda q: autotune[q])
             args.pieces = int(best)

@@ -152,12 +152,17 @@ def main() -> None:
             buckets.append(bk)
         backend = bc.BaguaCommBackendPy(nb, 0)
         backend.register_ordered_buckets(list(reversed(buckets)))
+        # the ready events must outlive the scheduled executions that wait for them (the
+        # scheduler keeps the raw handle, as the reference's BaguaTensor does)
+        events = []
         for b in reversed(range(nb)):
             ev = torch.cuda.Event()
             ev.record()
+            events.append(ev)
             for t in tensors[b]:
                 backend.mark_communication_ready(t, ev.cuda_event)
         done = backend.wait_pending_comm_ops()
+        del events
         assert done == nb, done
         out = {f"b{b}": _host(f) for b, f in enumerate(flats)}
         comm.barrier()

@@ -190,3 +190,25 @@ def test_op_captured_into_a_hip_graph(bc, comm, oracle_c, method):
         assert N.C.bagua_pool_bytes_in_use(0) == in_use
     finally:
         assert N.C.bagua_comm_set_async(comm.handle, 0) == 0
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("unfused", [False, True])
+def test_decentralized_p1_reads_its_own_bytes(bc, comm, oracle_c, dtype, unfused):
+    """One rank is its own left and right peer: the op reads its own payload in
+    place of the self send/recv (decentralized_low_precision_synchronous.rs:98-115
+    would deliver exactly those bytes), fused and reference sequence alike."""
+    N = bc._native
+    rng = np.random.default_rng(57 + dtype + 2 * unfused)
+    n = 1 << 16
+    arrs = [NP.from_f32((rng.standard_normal(n) * 1e-3).astype(np.float32), dtype) for _ in range(4)]
+    want = simulate.decentralized_low_precision(oracle_c, [arrs[0]], [arrs[1]], [arrs[2]], [arrs[3]], dtype)
+    ts = [dev(a, dtype) for a in arrs]
+    raws = [bc.BaguaTensorPy(x, nm).raw() for x, nm in zip(ts, "twlr")]
+    torch.cuda.synchronize()
+    fn = (N.C.bagua_decentralized_low_precision_synchronous_unfused if unfused
+          else N.C.bagua_decentralized_low_precision_synchronous)
+    N.check(fn(comm.handle, *[ctypes.byref(r) for r in raws], N.COMPRESSION_MINMAX_UINT8), "ring op")
+    comm.synchronize()
+    for got, w in zip(ts, want):
+        assert np.array_equal(host(got, dtype).view(np.uint8), w[0].view(np.uint8))
