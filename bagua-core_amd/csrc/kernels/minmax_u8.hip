@@ -364,18 +364,32 @@ int fused_blocks(int64_t cs, int per_vec);
 template <typename T>
 int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, int average, uint2* partials,
                         int blocks, hipStream_t s, int e0, int e1);
+template <typename T>
+int dequant_reduce_quantize_impl(const uint8_t* in, size_t in_bytes, int cs, int p, int average,
+                                 const uint2* partials, int npartials, uint8_t* seg, int64_t seg_bytes, int blocks,
+                                 hipStream_t s);
 
 template <typename T>
 static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, void* tensor, int average,
                                   uint8_t* out, size_t out_bytes, int target, void* ws, size_t ws_bytes,
                                   hipStream_t s) {
     using S = typename T::storage;
-    if (p <= 0 || p > kMaxFusedChunks || cs < 0 || target < 0 || target >= p || !tensor || !out)
+    if (p <= 0 || p > kMaxFusedChunks || cs < 0 || target < 0 || target >= p || !out)
         return BAGUA_ERR_UNSUPPORTED;
     const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     const int blocks = fused_blocks(cs, Vec<T>::N);
     if (!ws || ws_bytes < (size_t)blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
+    if (!tensor) {
+        // the reduced chunk is not stored: a partials-only pass, then the requantise
+        // recomputes it from the p received segments (p*cs bytes read twice instead of
+        // cs*sizeof(T) written and read back)
+        uint2* partials = static_cast<uint2*>(ws);
+        int rc = dequant_reduce_impl<T>(recv, recv_bytes, cs, p, nullptr, average, partials, blocks, s, 0, cs);
+        if (rc) return rc;
+        return dequant_reduce_quantize_impl<T>(recv, recv_bytes, cs, p, average, partials, blocks,
+                                               out + (int64_t)target * chunk_offset, chunk_offset, blocks, s);
+    }
     S* chunk = static_cast<S*>(tensor) + (int64_t)target * cs;
     uint2* partials = static_cast<uint2*>(ws);
     int rc = dequant_reduce_impl<T>(recv, recv_bytes, cs, p, chunk, average, partials, blocks, s, 0, cs);

@@ -22,16 +22,29 @@
 
 namespace bagua {
 
+// K:152-169 __from_float: the mean is a / n.  For n = 2^k the reciprocal is exact,
+// so a * 2^-k is the same correctly rounded value as a / 2^k (also for NaN, +-inf,
+// +-0 and denormal results): one multiply instead of a correctly rounded division
+// (~10 VALU ops per element).  AV: 0 = sum, 1 = / p, 2 = * (1/p) for p = 2^k.
+template <int AV>
+__device__ __forceinline__ float avg_finish(float s, float pf, float inv) {
+    if constexpr (AV == 0) return s;
+    else if constexpr (AV == 1) return s / pf;
+    else return s * inv;
+}
+inline int avg_mode(int average, int p) { return !average ? 0 : (p > 0 && (p & (p - 1)) == 0) ? 2 : 1; }
+
 
 
 // ---------------------------------------------------------------- plain ----
-template <typename T, int BY, bool AVG, bool VEC>
+template <typename T, int BY, int AV, bool VEC>
 __global__ __launch_bounds__(kBlock) void reduce_chunks_kernel(typename T::storage* __restrict__ x,
                                                                 int64_t cs, int p, int target) {
     using S = typename T::storage;
     constexpr int N = VEC ? Vec<T>::N : 1;
     const int64_t nitems = VEC ? cs / N : cs;
     const float pf = (float)p;
+    const float inv = 1.0f / pf;  // exact when AV == 2
     S* dst = x + (int64_t)target * cs;
     for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nitems; v += (int64_t)gridDim.x * kBlock) {
         float s[N][BY];
@@ -59,7 +72,7 @@ __global__ __launch_bounds__(kBlock) void reduce_chunks_kernel(typename T::stora
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             tree_finish<BY>(s[i]);
-            o[i] = AVG ? s[i][0] / pf : s[i][0];  // K:152-169 __from_float: a / n
+            o[i] = avg_finish<AV>(s[i][0], pf, inv);  // K:152-169 __from_float: a / n
         }
         if constexpr (VEC) {
             float f[Vec<T>::N];
@@ -81,13 +94,13 @@ __global__ __launch_bounds__(kBlock) void reduce_chunks_kernel(typename T::stora
                 s[y] = s[y] + T::to_f(x[(int64_t)c * cs + j]);
             }
             tree_finish<BY>(s);
-            dst[j] = T::from_f(AVG ? s[0] / pf : s[0]);
+            dst[j] = T::from_f(avg_finish<AV>(s[0], pf, inv));
         }
     }
 }
 
 
-template <typename T, int BY, bool AVG>
+template <typename T, int BY, int AV>
 static void launch_reduce(typename T::storage* x, int64_t cs, int p, int target, hipStream_t s) {
     // one lane keeps N x BY partial sums in registers: vectorise only while that stays small
     constexpr bool kVecFits = Vec<T>::N * BY <= 64;
@@ -99,22 +112,22 @@ static void launch_reduce(typename T::storage* x, int64_t cs, int p, int target,
     if (blocks < 1) blocks = 1;
     if constexpr (kVecFits) {
         if (vec) {
-            launch((reduce_chunks_kernel<T, BY, AVG, true>), dim3(blocks), dim3(kBlock), 0, s, x, cs, p,
+            launch((reduce_chunks_kernel<T, BY, AV, true>), dim3(blocks), dim3(kBlock), 0, s, x, cs, p,
                                target);
             return;
         }
     }
-        launch((reduce_chunks_kernel<T, BY, AVG, false>), dim3(blocks), dim3(kBlock), 0, s, x, cs, p, target);
+        launch((reduce_chunks_kernel<T, BY, AV, false>), dim3(blocks), dim3(kBlock), 0, s, x, cs, p, target);
 }
 
-template <typename T, bool AVG>
+template <typename T, int AV>
 static void dispatch_reduce(typename T::storage* x, int64_t cs, int p, int target, hipStream_t s) {
     switch (reduce_by(p)) {
-        case 2: launch_reduce<T, 2, AVG>(x, cs, p, target, s); break;
-        case 4: launch_reduce<T, 4, AVG>(x, cs, p, target, s); break;
-        case 8: launch_reduce<T, 8, AVG>(x, cs, p, target, s); break;
-        case 16: launch_reduce<T, 16, AVG>(x, cs, p, target, s); break;
-        default: launch_reduce<T, 32, AVG>(x, cs, p, target, s); break;
+        case 2: launch_reduce<T, 2, AV>(x, cs, p, target, s); break;
+        case 4: launch_reduce<T, 4, AV>(x, cs, p, target, s); break;
+        case 8: launch_reduce<T, 8, AV>(x, cs, p, target, s); break;
+        case 16: launch_reduce<T, 16, AV>(x, cs, p, target, s); break;
+        default: launch_reduce<T, 32, AV>(x, cs, p, target, s); break;
     }
 }
 
@@ -122,8 +135,11 @@ template <typename T>
 static int reduce_impl(void* x, int cs, int p, int target, int average, hipStream_t s) {
     if (!x || cs < 0 || p <= 0 || target < 0 || target >= p) return BAGUA_ERR_INVALID_ARG;
     using S = typename T::storage;
-    if (average) dispatch_reduce<T, true>(static_cast<S*>(x), cs, p, target, s);
-    else dispatch_reduce<T, false>(static_cast<S*>(x), cs, p, target, s);
+    switch (avg_mode(average, p)) {
+        case 0: dispatch_reduce<T, 0>(static_cast<S*>(x), cs, p, target, s); break;
+        case 1: dispatch_reduce<T, 1>(static_cast<S*>(x), cs, p, target, s); break;
+        default: dispatch_reduce<T, 2>(static_cast<S*>(x), cs, p, target, s); break;
+    }
     return check_launch();
 }
 
@@ -138,15 +154,13 @@ constexpr int fused_q() {
     return (64 / (Vec<T>::N * BY)) < 1 ? 1 : 64 / (Vec<T>::N * BY);
 }
 
-template <typename T, int BY, bool AVG, bool PARTIALS>
-__global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
-    const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t e0, int64_t cs, int p,
-    typename T::storage* __restrict__ out, uint2* __restrict__ partials) {
-    // reduces elements [e0, e0 + cs) of the chunk (`out` points at element e0)
+// dequantisation tables of the p segments in LDS: lut[c][b] = byte b of segment
+// c dequantised and rounded to T, as the reference stores it before reducing
+// (codec_common.hpp "dequantisation tables")
+template <typename T>
+__device__ __forceinline__ void build_luts(const uint8_t* in, int64_t chunk_offset, int p, QParams* qp,
+                                           float (*lut)[256]) {
     using S = typename T::storage;
-    constexpr int N = Vec<T>::N;
-    constexpr int Q = fused_q<T, BY>();
-    __shared__ QParams qp[kMaxFusedChunks];
     for (int c = threadIdx.x; c < p; c += kBlock) {
         const uint8_t* seg = in + (int64_t)c * chunk_offset;
         S hmn, hmx;
@@ -155,16 +169,27 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
         qp[c] = make_qparams(T::to_f(hmn), T::to_f(hmx));
     }
     __syncthreads();
-    // dequantised value of every byte of every segment, as the reference stores
-    // it in T before reducing (codec_common.hpp "dequantisation tables")
-    __shared__ float lut[kMaxFusedChunks][256];
     for (int i = threadIdx.x; i < p * 256; i += kBlock) lut[i >> 8][i & 255] = as_stored<T>(dequant(i & 255, qp[i >> 8]));
     __syncthreads();
+}
+
+// The reduced chunk, tile by tile: every full 16-B vector v of the result goes
+// to vec(v, packed T vector), each element j of the ragged tail (< N elements,
+// workgroup 0) to tail(j, value rounded to T).  `base` = payload byte e0 of
+// segment 0.  Summation follows the reference's tree order (block_y_reduce,
+// K:171-194), then / p for the mean (K:152-169 __from_float).
+// PF > 0: p is known at compile time (PF = 1: no second, duplicate load per vector
+// for the BY = 2 tree of a single segment)
+template <typename T, int BY, int AV, int PF, typename VecF, typename TailF>
+__device__ __forceinline__ void reduce_tiles(const uint8_t* base, int64_t chunk_offset, int64_t cs, int p_rt,
+                                             const float (*lut)[256], VecF&& vec, TailF&& tail) {
+    const int p = PF > 0 ? PF : p_rt;
+    constexpr int N = Vec<T>::N;
+    constexpr int Q = fused_q<T, BY>();
     const float pf = (float)p;
-    uint32_t lo = min_space(T::init_max()), hi = max_space(-T::init_max());
-    // fast path: every segment's payload N-byte aligned and out 16-B aligned (checked on host)
+    const float inv = 1.0f / pf;  // exact when AV == 2
+    // fast path: every segment's payload N-byte aligned (checked on host)
     const int64_t nvec = cs / N;
-    const uint8_t* base = in + 32 + e0;
     for (int64_t tile = (int64_t)blockIdx.x * kBlock * Q; tile < nvec; tile += (int64_t)gridDim.x * kBlock * Q) {
         const bool full = tile + (int64_t)kBlock * Q <= nvec;
         float s[Q][N][BY];
@@ -216,21 +241,9 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
 #pragma unroll
             for (int i = 0; i < N; ++i) {
                 tree_finish<BY>(s[q][i]);
-                o[i] = AVG ? s[q][i][0] / pf : s[q][i][0];
+                o[i] = avg_finish<AV>(s[q][i][0], pf, inv);
             }
-            const uint4 packed = pack16<T>(o);
-            *reinterpret_cast<uint4*>(out + v * N) = packed;
-            if constexpr (PARTIALS) {
-                // min/max of the values as stored in T (what the requantiser reads back)
-                float st[N];
-                unpack16<T>(packed, st);
-#pragma unroll
-                for (int i = 0; i < N; ++i) {
-                    const int32_t k = f2key(st[i]);  // NaN wraps to a huge key in both spaces
-                    lo = min(lo, min_space_key(k));
-                    hi = min(hi, max_space_key(k));
-                }
-            }
+            vec(v, pack16<T>(o));
         }
     }
     if (blockIdx.x == 0 && threadIdx.x < cs - nvec * N) {  // ragged tail (< N elements)
@@ -243,47 +256,176 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
             s[y] = s[y] + lut[c][base[(int64_t)c * chunk_offset + j]];
         }
         tree_finish<BY>(s);
-        const S o = T::from_f(AVG ? s[0] / pf : s[0]);
-        out[j] = o;
-        if constexpr (PARTIALS) {
-            const int32_t k = f2key(T::to_f(o));
-            lo = min(lo, min_space_key(k));
-            hi = min(hi, max_space_key(k));
-        }
-    }
-    if constexpr (PARTIALS) {
-        lo = wave_umin(lo);
-        hi = wave_umin(hi);
-        __shared__ uint32_t red[2][kWavesPerBlock];
-        const int w = threadIdx.x / kWave;
-        if (lane_id() == 0) { red[0][w] = lo; red[1][w] = hi; }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-#pragma unroll
-            for (int i = 1; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
-            partials[blockIdx.x] = make_uint2(lo, hi);
-        }
+        tail(j, T::from_f(avg_finish<AV>(s[0], pf, inv)));
     }
 }
 
-template <typename T, int BY, bool AVG>
+// the workgroup's {min, max} keys -> partials[blockIdx.x]
+__device__ __forceinline__ void store_block_partial(uint32_t lo, uint32_t hi, uint2* partials) {
+    lo = wave_umin(lo);
+    hi = wave_umin(hi);
+    __shared__ uint32_t red[2][kWavesPerBlock];
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 0) { red[0][w] = lo; red[1][w] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 1; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
+        partials[blockIdx.x] = make_uint2(lo, hi);
+    }
+}
+
+// STORE: write the reduced chunk to `out`; PARTIALS: emit the min/max partials of
+// its values as stored in T (what the requantiser reads back).  !STORE needs
+// PARTIALS: the requantise then recomputes the values (dequant_reduce_quantize_kernel).
+template <typename T, int BY, int AV, bool PARTIALS, bool STORE = true, int PF = 0>
+__global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
+    const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t e0, int64_t cs, int p,
+    typename T::storage* __restrict__ out, uint2* __restrict__ partials) {
+    // reduces elements [e0, e0 + cs) of the chunk (`out` points at element e0)
+    using S = typename T::storage;
+    constexpr int N = Vec<T>::N;
+    static_assert(STORE || PARTIALS, "a pass that neither stores nor reduces does nothing");
+    __shared__ QParams qp[kMaxFusedChunks];
+    __shared__ float lut[kMaxFusedChunks][256];
+    build_luts<T>(in, chunk_offset, p, qp, lut);
+    uint32_t lo = min_space(T::init_max()), hi = max_space(-T::init_max());
+    reduce_tiles<T, BY, AV, PF>(
+        in + 32 + e0, chunk_offset, cs, p, lut,
+        [&](int64_t v, const uint4& packed) {
+            if constexpr (STORE) *reinterpret_cast<uint4*>(out + v * N) = packed;
+            if constexpr (PARTIALS) {
+                float st[N];
+                unpack16<T>(packed, st);
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    const int32_t k = f2key(st[i]);  // NaN wraps to a huge key in both spaces
+                    lo = min(lo, min_space_key(k));
+                    hi = min(hi, max_space_key(k));
+                }
+            }
+        },
+        [&](int64_t j, S o) {
+            if constexpr (STORE) out[j] = o;
+            if constexpr (PARTIALS) {
+                const int32_t k = f2key(T::to_f(o));
+                lo = min(lo, min_space_key(k));
+                hi = min(hi, max_space_key(k));
+            }
+        });
+    if constexpr (PARTIALS) store_block_partial(lo, hi, partials);
+}
+
+// Requantise the own chunk without reading a stored copy of it: fold the min/max
+// partials the partials-only pass emitted, then recompute every reduced value from
+// the p received segments (the same LDS tables and summation tree, so the same T
+// values bit for bit) and quantise it into the payload of segment `seg` (header and
+// slack included) -- the bytes minmax_quantize_kernel writes from the stored chunk.
+// Reads p*cs payload bytes instead of the stored chunk's cs*sizeof(T) (and saves its
+// write), so it pays for p < 2*sizeof(T).
+template <typename T, int BY, int AV, int PF = 0>
+__global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
+    const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int p, const uint2* __restrict__ partials,
+    int npartials, uint8_t* __restrict__ seg, int64_t seg_bytes) {
+    using S = typename T::storage;
+    constexpr int N = Vec<T>::N;
+    __shared__ QParams qp[kMaxFusedChunks];
+    __shared__ float lut[kMaxFusedChunks][256];
+    uint32_t lo = 0xffffffffu, hi = 0xffffffffu;
+    for (int i = threadIdx.x; i < npartials; i += kBlock) {
+        const uint2 pr = partials[i];
+        lo = min(lo, pr.x);
+        hi = min(hi, pr.y);
+    }
+    lo = wave_umin(lo);
+    hi = wave_umin(hi);
+    __shared__ uint32_t red[2][kWavesPerBlock];
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 0) { red[0][w] = lo; red[1][w] = hi; }
+    build_luts<T>(in, chunk_offset, p, qp, lut);  // its barriers publish red[][] too
+#pragma unroll
+    for (int i = 0; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
+    const float mn = from_min_space(lo), mx = from_max_space(hi);  // exact in T (header, K:462-463)
+    const QParams q = make_qparams(mn, mx);
+    if (blockIdx.x == 0) {
+        const int t = threadIdx.x;
+        if (t < 32) {  // header {T min, T max, zero gap}
+            const uint32_t bmn = sizeof(S) == 4 ? __float_as_uint(mn) : (uint32_t)T::from_f(mn);
+            const uint32_t bmx = sizeof(S) == 4 ? __float_as_uint(mx) : (uint32_t)T::from_f(mx);
+            uint32_t hb = 0;
+            if (t < (int)sizeof(S)) hb = (bmn >> (8 * t)) & 0xff;
+            else if (t < 2 * (int)sizeof(S)) hb = (bmx >> (8 * (t - (int)sizeof(S)))) & 0xff;
+            seg[t] = (uint8_t)hb;
+        }
+        for (int64_t j = 32 + cs + t; j < seg_bytes; j += kBlock) seg[j] = 0;  // slack
+    }
+    uint8_t* payload = seg + 32;
+    reduce_tiles<T, BY, AV, PF>(
+        in + 32, chunk_offset, cs, p, lut,
+        [&](int64_t v, const uint4& packed) {
+            float st[N];
+            unpack16<T>(packed, st);
+            quant_store_vec<T>(st, q, payload + v * N);
+        },
+        [&](int64_t j, S o) { payload[j] = (uint8_t)quant(T::to_f(o), q); });
+}
+
+template <typename T, int BY, int AV>
 static void launch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, int p, typename T::storage* out,
                          uint2* partials, int blocks, hipStream_t s) {
-    if (partials)
-        launch((dequant_reduce_kernel<T, BY, AVG, true>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
+    // out == nullptr: partials only (the requantise recomputes the chunk)
+    if (p == 1 && BY == 2) {
+        if (!out)
+            launch((dequant_reduce_kernel<T, 2, AV, true, false, 1>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
+                   cs, p, out, partials);
+        else if (partials)
+            launch((dequant_reduce_kernel<T, 2, AV, true, true, 1>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
+                   cs, p, out, partials);
+        else
+            launch((dequant_reduce_kernel<T, 2, AV, false, true, 1>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
+                   cs, p, out, partials);
+    } else if (!out)
+        launch((dequant_reduce_kernel<T, BY, AV, true, false>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0, cs, p,
+               out, partials);
+    else if (partials)
+        launch((dequant_reduce_kernel<T, BY, AV, true>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
                            cs, p, out, partials);
     else
-        launch((dequant_reduce_kernel<T, BY, AVG, false>), dim3(blocks), dim3(kBlock), 0, s, in, co,
+        launch((dequant_reduce_kernel<T, BY, AV, false>), dim3(blocks), dim3(kBlock), 0, s, in, co,
                            e0, cs, p, out, partials);
 }
 
-template <typename T, bool AVG>
+template <typename T, int AV>
 static void dispatch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, int p, typename T::storage* out,
                            uint2* partials, int blocks, hipStream_t s) {
     switch (reduce_by(p)) {  // p <= kMaxFusedChunks (16) keeps BY <= 8
-        case 2: launch_fused<T, 2, AVG>(in, co, e0, cs, p, out, partials, blocks, s); break;
-        case 4: launch_fused<T, 4, AVG>(in, co, e0, cs, p, out, partials, blocks, s); break;
-        default: launch_fused<T, 8, AVG>(in, co, e0, cs, p, out, partials, blocks, s); break;
+        case 2: launch_fused<T, 2, AV>(in, co, e0, cs, p, out, partials, blocks, s); break;
+        case 4: launch_fused<T, 4, AV>(in, co, e0, cs, p, out, partials, blocks, s); break;
+        default: launch_fused<T, 8, AV>(in, co, e0, cs, p, out, partials, blocks, s); break;
+    }
+}
+
+template <typename T, int AV>
+static void dispatch_reduce_quantize(const uint8_t* in, int64_t co, int64_t cs, int p, const uint2* partials,
+                                     int npartials, uint8_t* seg, int64_t seg_bytes, int blocks, hipStream_t s) {
+    if (p == 1) {
+        launch((dequant_reduce_quantize_kernel<T, 2, AV, 1>), dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
+               partials, npartials, seg, seg_bytes);
+        return;
+    }
+    switch (reduce_by(p)) {
+        case 2:
+            launch((dequant_reduce_quantize_kernel<T, 2, AV>), dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
+                   partials, npartials, seg, seg_bytes);
+            break;
+        case 4:
+            launch((dequant_reduce_quantize_kernel<T, 4, AV>), dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
+                   partials, npartials, seg, seg_bytes);
+            break;
+        default:
+            launch((dequant_reduce_quantize_kernel<T, 8, AV>), dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
+                   partials, npartials, seg, seg_bytes);
+            break;
     }
 }
 
@@ -296,25 +438,57 @@ int fused_blocks(int64_t cs, int per_vec) {
 template <typename T>
 int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, int average,
                         uint2* partials, int blocks, hipStream_t s, int e0, int e1) {
-    // reduces elements [e0, e1) of the chunk whose element 0 is at `out`
+    // reduces elements [e0, e1) of the chunk whose element 0 is at `out`;
+    // out == nullptr: partials only (nothing stored)
     using S = typename T::storage;
-    if (!in || !out || cs < 0 || p <= 0 || e0 < 0 || e1 < e0 || e1 > cs) return BAGUA_ERR_INVALID_ARG;
+    if (!in || (!out && !partials) || cs < 0 || p <= 0 || e0 < 0 || e1 < e0 || e1 > cs) return BAGUA_ERR_INVALID_ARG;
     if (p > kMaxFusedChunks) return BAGUA_ERR_UNSUPPORTED;  // caller falls back to decompress + reduce
     const int64_t co = (int64_t)(in_bytes / (size_t)p);
     if (co < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     constexpr int N = Vec<T>::N;
     // vector path: out 16-B aligned and every segment payload N-byte aligned
-    S* o = static_cast<S*>(out) + e0;
+    S* o = out ? static_cast<S*>(out) + e0 : nullptr;
     const bool aligned = ((uintptr_t)o % 16 == 0) && (((uintptr_t)in + 32 + e0) % N == 0) && (co % N == 0);
     if (!aligned) return BAGUA_ERR_UNSUPPORTED;  // caller falls back to decompress + reduce
-    if (average) dispatch_fused<T, true>(in, co, e0, e1 - e0, p, o, partials, blocks, s);
-    else dispatch_fused<T, false>(in, co, e0, e1 - e0, p, o, partials, blocks, s);
+    switch (avg_mode(average, p)) {
+        case 0: dispatch_fused<T, 0>(in, co, e0, e1 - e0, p, o, partials, blocks, s); break;
+        case 1: dispatch_fused<T, 1>(in, co, e0, e1 - e0, p, o, partials, blocks, s); break;
+        default: dispatch_fused<T, 2>(in, co, e0, e1 - e0, p, o, partials, blocks, s); break;
+    }
+    return check_launch();
+}
+
+// quantise the reduced chunk, recomputed from the p received segments, into `seg`
+// (seg_bytes: the segment incl. header and slack), after dequant_reduce_impl with
+// out == nullptr emitted `npartials` partials (the same `blocks`)
+template <typename T>
+int dequant_reduce_quantize_impl(const uint8_t* in, size_t in_bytes, int cs, int p, int average,
+                                 const uint2* partials, int npartials, uint8_t* seg, int64_t seg_bytes, int blocks,
+                                 hipStream_t s) {
+    if (!in || !partials || !seg || cs < 0 || p <= 0 || npartials < 1) return BAGUA_ERR_INVALID_ARG;
+    if (p > kMaxFusedChunks) return BAGUA_ERR_UNSUPPORTED;
+    const int64_t co = (int64_t)(in_bytes / (size_t)p);
+    if (co < (int64_t)cs + 32 || seg_bytes < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
+    constexpr int N = Vec<T>::N;
+    const bool aligned = (((uintptr_t)in + 32) % N == 0) && (co % N == 0) && (((uintptr_t)seg + 32) % N == 0);
+    if (!aligned) return BAGUA_ERR_UNSUPPORTED;
+    switch (avg_mode(average, p)) {
+        case 0: dispatch_reduce_quantize<T, 0>(in, co, cs, p, partials, npartials, seg, seg_bytes, blocks, s); break;
+        case 1: dispatch_reduce_quantize<T, 1>(in, co, cs, p, partials, npartials, seg, seg_bytes, blocks, s); break;
+        default: dispatch_reduce_quantize<T, 2>(in, co, cs, p, partials, npartials, seg, seg_bytes, blocks, s); break;
+    }
     return check_launch();
 }
 
 template int dequant_reduce_impl<F32>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
 template int dequant_reduce_impl<F16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
 template int dequant_reduce_impl<BF16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
+template int dequant_reduce_quantize_impl<F32>(const uint8_t*, size_t, int, int, int, const uint2*, int, uint8_t*,
+                                               int64_t, int, hipStream_t);
+template int dequant_reduce_quantize_impl<F16>(const uint8_t*, size_t, int, int, int, const uint2*, int, uint8_t*,
+                                               int64_t, int, hipStream_t);
+template int dequant_reduce_quantize_impl<BF16>(const uint8_t*, size_t, int, int, int, const uint2*, int, uint8_t*,
+                                                int64_t, int, hipStream_t);
 
 }  // namespace bagua
 

@@ -112,6 +112,8 @@ class OpBuffer {
         if (rc) return finish(c, rc); \
     } while (0)
 
+int env_int(const char* name, long dflt);
+
 int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int average, int method, bool fused) {
     Chunking k;
     int rc = plan(c, t, method, &k);
@@ -147,9 +149,16 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
         const size_t ws_bytes = bagua_minmax_u8_workspace_bytes((int)k.cs, k.p);
         const uint64_t ws = stream_workspace(c->device_id, s, ws_bytes);
         if (!ws) return finish(c, BAGUA_ERR_OOM);
+        // the reduced chunk is dead (step 5's decompress rewrites every element): below
+        // p = 2*sizeof(T) recomputing it from the p received segments moves fewer bytes
+        // than storing it and reading it back (p*cs vs 2*cs*sizeof(T); p = 1: 10 -> 3 bytes
+        // per element); BAGUA_REDUCE_RECOMPUTE=0/1 forces either way (A/B)
+        const int rcm = env_int("BAGUA_REDUCE_RECOMPUTE", -1);
+        const bool recompute = rcm >= 0 ? rcm != 0 : (size_t)k.p < 2 * bagua_dtype_bytes(t->dtype);
         rc = bagua_minmax_u8_reduce_requantize(t->dtype, rbuf, k.S, (int)k.cs, k.p,
-                                               (void*)(uintptr_t)t->ptr, average, send.as<uint8_t>(), k.S, k.rank,
-                                               (void*)(uintptr_t)ws, ws_bytes, (void*)(uintptr_t)s);
+                                               recompute ? nullptr : (void*)(uintptr_t)t->ptr, average,
+                                               send.as<uint8_t>(), k.S, k.rank, (void*)(uintptr_t)ws, ws_bytes,
+                                               (void*)(uintptr_t)s);
         if (rc == BAGUA_OK) done = true;
         else if (rc != BAGUA_ERR_UNSUPPORTED) return finish(c, rc);
     } else if (fused && method == BAGUA_COMPRESSION_ONEBIT && t->num_elem == t->num_elem_allocated) {

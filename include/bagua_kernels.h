@@ -163,7 +163,13 @@ int bagua_minmax_u8_decompress_reduce(int dtype, const uint8_t* input, size_t in
  * requantise that chunk into segment `target_chunk` of `output` (a
  * num_chunks-segment MinMax-UInt8 buffer of output_bytes).  Bit-identical to
  * the unfused sequence.  Returns BAGUA_ERR_UNSUPPORTED when the shape has no
- * vector path (num_chunks > 16 or misaligned); callers then run the unfused ops. */
+ * vector path (num_chunks > 16 or misaligned); callers then run the unfused ops.
+ * `tensor` may be NULL: the reduced chunk is then not stored (the centralized
+ * op overwrites it with its final decompress anyway); a partials-only pass is
+ * followed by a requantise that recomputes the reduced values from `input`
+ * (same bytes; 2*num_chunks*chunk_size payload bytes read instead of
+ * num_chunks*chunk_size + 2*chunk_size*sizeof(T) moved, so it pays for
+ * num_chunks < 2*sizeof(T)). */
 int bagua_minmax_u8_reduce_requantize(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
                                       int num_chunks, void* tensor, int average, uint8_t* output,
                                       size_t output_bytes, int target_chunk, void* workspace,

@@ -193,12 +193,17 @@ def test_reduce_goldens(bc, goldens):
 
 
 @pytest.mark.parametrize("dtype", [F32, F16, BF16])
-@pytest.mark.parametrize("p", [1, 2, 3, 4, 8, 12, 16])
-def test_fused_reduce_requantize(bc, oracle_c, dtype, p):
-    """bagua_minmax_u8_reduce_requantize == decompress_from + reduce_mean + compress(target)."""
+@pytest.mark.parametrize("p,ragged", [(1, 0), (2, 0), (3, 0), (4, 0), (8, 0), (12, 0), (16, 0), (1, 3), (2, 5),
+                                      (4, 1)])
+@pytest.mark.parametrize("store", [True, False])
+@pytest.mark.parametrize("average", [1, 0])
+def test_fused_reduce_requantize(bc, oracle_c, dtype, p, ragged, store, average):
+    """bagua_minmax_u8_reduce_requantize == decompress_from + reduce_{mean,sum} + compress(target);
+    with a NULL tensor (the reduced chunk recomputed, never stored) the same segment bytes and
+    nothing of the tensor written."""
     from oracle import oracle_np as NP
     rng = np.random.default_rng(100 + p + dtype)
-    cs = 40000 + 8 * p
+    cs = 40000 + 8 * p + ragged  # ragged: a tail of < one 16-B vector of elements
     xs = [NP.from_f32((rng.standard_normal(p * cs) * 1e-3).astype(np.float32), dtype) for _ in range(p)]
     # the alltoall receive buffer of rank `r`: slot j = rank j's segment r
     r = p // 2
@@ -209,21 +214,31 @@ def test_fused_reduce_requantize(bc, oracle_c, dtype, p):
     # oracle: decompress, reduce into chunk r, compress target r
     t_want = np.zeros(p * cs, STORAGE[dtype])
     oracle_c.decompress_minmax_u8(recv, p, t_want, dtype)
-    oracle_c.reduce_chunks(t_want, dtype, p, r, True)
+    oracle_c.reduce_chunks(t_want, dtype, p, r, bool(average))
     send_want = np.zeros(S, np.uint8)
     oracle_c.compress_minmax_u8(t_want, dtype, p, r, out=send_want)
-    # GPU
+    # GPU (segments are poisoned: header gap and slack must be written as zeros)
     K = bc._native.K
     recv_d = torch.from_numpy(recv).cuda()
-    t_d = torch.zeros(p * cs, dtype=TORCH[dtype], device="cuda")
-    send_d = torch.zeros(S, dtype=torch.uint8, device="cuda")
+    t_d = torch.full((p * cs,), 7.0, dtype=TORCH[dtype], device="cuda")
+    send_d = torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
     ws = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
-    rc = K.bagua_minmax_u8_reduce_requantize(dtype, recv_d.data_ptr(), S, cs, p, t_d.data_ptr(), 1,
-                                             send_d.data_ptr(), S, r, ws.data_ptr(), ws.numel(), None)
+    rc = K.bagua_minmax_u8_reduce_requantize(dtype, recv_d.data_ptr(), S, cs, p, t_d.data_ptr() if store else None,
+                                             average, send_d.data_ptr(), S, r, ws.data_ptr(), ws.numel(), None)
+    if store and (r * cs * t_d.element_size()) % 16:
+        assert rc == 4  # BAGUA_ERR_UNSUPPORTED: no vector path into a misaligned chunk (callers run unfused)
+        return
     assert rc == 0
     got_t = to_host(t_d, dtype)
-    assert_float_bits_equal(got_t[r * cs:(r + 1) * cs], t_want[r * cs:(r + 1) * cs], dtype, "reduced chunk")
-    assert np.array_equal(segment_bytes(send_d.cpu().numpy(), p, r), segment_bytes(send_want, p, r))
+    if store:
+        assert_float_bits_equal(got_t[r * cs:(r + 1) * cs], t_want[r * cs:(r + 1) * cs], dtype, "reduced chunk")
+    else:
+        assert np.all(got_t.astype(np.float32) == 7.0) if dtype != BF16 else np.all(got_t == 0x40E0)
+    got = send_d.cpu().numpy()
+    assert np.array_equal(got[r * co:(r + 1) * co], send_want[r * co:(r + 1) * co])
+    other = np.ones(S, bool)
+    other[r * co:(r + 1) * co] = False
+    assert np.all(got[other] == 0xA5), "bytes outside the target segment written"
 
 
 # ---------------------------------------------------------------- 1-bit -----
