@@ -83,6 +83,8 @@ KERNEL_SIGNATURES = {
     "bagua_minmax_u8_decompress_reduce": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _vp]),
     "bagua_minmax_u8_reduce_requantize": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _vp, _sz, _i32, _vp, _sz,
                                                  _vp]),
+    "bagua_minmax_u8_reduce_requantize_final": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _vp, _sz, _i32, _vp,
+                                                       _sz, _vp]),
     "bagua_minmax_u8_piece_range": (_i32, [_i32, _i32, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
     "bagua_minmax_u8_pipeline_workspace_bytes": (_sz, [_i32, _i32]),
     "bagua_minmax_u8_quantize_range": (_i32, [_i32, _vp, _i32, _i32, _i32, _vp, _sz, _vp, _sz, _i32, _i32, _i32,

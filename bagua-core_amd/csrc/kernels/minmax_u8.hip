@@ -367,17 +367,18 @@ int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void*
 template <typename T>
 int dequant_reduce_quantize_impl(const uint8_t* in, size_t in_bytes, int cs, int p, int average,
                                  const uint2* partials, int npartials, uint8_t* seg, int64_t seg_bytes, int blocks,
-                                 hipStream_t s);
+                                 hipStream_t s, void* final_chunk);
 
 template <typename T>
 static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, void* tensor, int average,
                                   uint8_t* out, size_t out_bytes, int target, void* ws, size_t ws_bytes,
-                                  hipStream_t s) {
+                                  hipStream_t s, void* final_tensor = nullptr) {
     using S = typename T::storage;
-    if (p <= 0 || p > kMaxFusedChunks || cs < 0 || target < 0 || target >= p || !out)
+    if (final_tensor) tensor = nullptr;  // the final decompress of the own chunk replaces the store
+    if (p <= 0 || p > kMaxFusedChunks || cs < 0 || target < 0 || target >= p || (!out && !final_tensor))
         return BAGUA_ERR_UNSUPPORTED;
     const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);
-    if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
+    if (out && chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     const int blocks = fused_blocks(cs, Vec<T>::N);
     if (!ws || ws_bytes < (size_t)blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
     if (!tensor) {
@@ -387,8 +388,10 @@ static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs
         uint2* partials = static_cast<uint2*>(ws);
         int rc = dequant_reduce_impl<T>(recv, recv_bytes, cs, p, nullptr, average, partials, blocks, s, 0, cs);
         if (rc) return rc;
-        return dequant_reduce_quantize_impl<T>(recv, recv_bytes, cs, p, average, partials, blocks,
-                                               out + (int64_t)target * chunk_offset, chunk_offset, blocks, s);
+        return dequant_reduce_quantize_impl<T>(
+            recv, recv_bytes, cs, p, average, partials, blocks, out ? out + (int64_t)target * chunk_offset : nullptr,
+            chunk_offset,
+            blocks, s, final_tensor ? static_cast<void*>(static_cast<S*>(final_tensor) + (int64_t)target * cs) : nullptr);
     }
     S* chunk = static_cast<S*>(tensor) + (int64_t)target * cs;
     uint2* partials = static_cast<uint2*>(ws);
@@ -574,6 +577,26 @@ int bagua_minmax_u8_reduce_requantize(int dtype, const uint8_t* input, size_t in
         case BAGUA_DTYPE_BF16:
             return reduce_requantize_impl<BF16>(input, input_bytes, chunk_size, num_chunks, tensor, average, output,
                                                 output_bytes, target_chunk, workspace, workspace_bytes, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+int bagua_minmax_u8_reduce_requantize_final(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                                            int num_chunks, void* tensor, int average, uint8_t* output,
+                                            size_t output_bytes, int target_chunk, void* workspace,
+                                            size_t workspace_bytes, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!tensor) return BAGUA_ERR_INVALID_ARG;
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return reduce_requantize_impl<F32>(input, input_bytes, chunk_size, num_chunks, nullptr, average, output,
+                                               output_bytes, target_chunk, workspace, workspace_bytes, s, tensor);
+        case BAGUA_DTYPE_F16:
+            return reduce_requantize_impl<F16>(input, input_bytes, chunk_size, num_chunks, nullptr, average, output,
+                                               output_bytes, target_chunk, workspace, workspace_bytes, s, tensor);
+        case BAGUA_DTYPE_BF16:
+            return reduce_requantize_impl<BF16>(input, input_bytes, chunk_size, num_chunks, nullptr, average, output,
+                                                output_bytes, target_chunk, workspace, workspace_bytes, s, tensor);
     }
     return BAGUA_ERR_UNSUPPORTED;
 }

@@ -323,10 +323,17 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
 // slack included) -- the bytes minmax_quantize_kernel writes from the stored chunk.
 // Reads p*cs payload bytes instead of the stored chunk's cs*sizeof(T) (and saves its
 // write), so it pays for p < 2*sizeof(T).
-template <typename T, int BY, int AV, int PF = 0>
+//
+// FINAL: also write the decompressed requantised chunk (what the op's final
+// decompress writes there, minmax_dequantize_kernel's table and nt stores) to
+// `final_out` -- one rank's op then needs no final decompress launch -- and, with
+// seg == nullptr, skip the segment (nothing reads it: one rank gathers nothing;
+// plain stores of it left 268 MB dirty in the Infinity Cache in front of the next
+// 1 GiB encode, +40 us, nt stores cost the kernel +76 us).
+template <typename T, int BY, int AV, int PF = 0, bool FINAL = false>
 __global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
     const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int p, const uint2* __restrict__ partials,
-    int npartials, uint8_t* __restrict__ seg, int64_t seg_bytes) {
+    int npartials, uint8_t* __restrict__ seg, int64_t seg_bytes, typename T::storage* __restrict__ final_out) {
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
     __shared__ QParams qp[kMaxFusedChunks];
@@ -347,7 +354,13 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
     for (int i = 0; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
     const float mn = from_min_space(lo), mx = from_max_space(hi);  // exact in T (header, K:462-463)
     const QParams q = make_qparams(mn, mx);
-    if (blockIdx.x == 0) {
+    __shared__ uint32_t lut2[FINAL ? 256 : 1];  // stored T bits of every byte value (the final decompress)
+    if constexpr (FINAL) {
+        static_assert(kBlock == 256, "one table entry per thread");
+        lut2[threadIdx.x] = stored_bits<T>(dequant(threadIdx.x, q));
+        __syncthreads();
+    }
+    if (blockIdx.x == 0 && (!FINAL || seg)) {
         const int t = threadIdx.x;
         if (t < 32) {  // header {T min, T max, zero gap}
             const uint32_t bmn = sizeof(S) == 4 ? __float_as_uint(mn) : (uint32_t)T::from_f(mn);
@@ -365,9 +378,25 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
         [&](int64_t v, const uint4& packed) {
             float st[N];
             unpack16<T>(packed, st);
-            quant_store_vec<T>(st, q, payload + v * N);
+            if constexpr (!FINAL) {
+                quant_store_vec<T>(st, q, payload + v * N);
+            } else {
+                typename Vec<T>::out_bytes w;
+                if constexpr (N == 4) w = quant_pack4(st[0], st[1], st[2], st[3], q);
+                else w = make_uint2(quant_pack4(st[0], st[1], st[2], st[3], q), quant_pack4(st[4], st[5], st[6], st[7], q));
+                if (seg) *reinterpret_cast<typename Vec<T>::out_bytes*>(payload + v * N) = w;  // plain (store_bytes)
+                uint32_t b[N];
+                split_bytes<T>(w, b);
+#pragma unroll
+                for (int i = 0; i < N; ++i) b[i] = lut2[b[i]];
+                nt_store16(pack_stored<T>(b), final_out + v * N);
+            }
         },
-        [&](int64_t j, S o) { payload[j] = (uint8_t)quant(T::to_f(o), q); });
+        [&](int64_t j, S o) {
+            const uint32_t b = quant(T::to_f(o), q);
+            if (!FINAL || seg) payload[j] = (uint8_t)b;
+            if constexpr (FINAL) final_out[j] = storage_from_bits<T>(lut2[b]);
+        });
 }
 
 template <typename T, int BY, int AV>
@@ -405,28 +434,45 @@ static void dispatch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs
     }
 }
 
-template <typename T, int AV>
-static void dispatch_reduce_quantize(const uint8_t* in, int64_t co, int64_t cs, int p, const uint2* partials,
-                                     int npartials, uint8_t* seg, int64_t seg_bytes, int blocks, hipStream_t s) {
-    if (p == 1) {
-        launch((dequant_reduce_quantize_kernel<T, 2, AV, 1>), dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
-               partials, npartials, seg, seg_bytes);
-        return;
-    }
-    switch (reduce_by(p)) {
+template <typename T, int AV, int PF, bool FINAL>
+static void launch_reduce_quantize(int by, const uint8_t* in, int64_t co, int64_t cs, int p, const uint2* partials,
+                                   int npartials, uint8_t* seg, int64_t seg_bytes, typename T::storage* final_out,
+                                   int blocks, hipStream_t s) {
+    switch (by) {
         case 2:
-            launch((dequant_reduce_quantize_kernel<T, 2, AV>), dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
-                   partials, npartials, seg, seg_bytes);
+            launch((dequant_reduce_quantize_kernel<T, 2, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
+                   cs, p, partials, npartials, seg, seg_bytes, final_out);
             break;
         case 4:
-            launch((dequant_reduce_quantize_kernel<T, 4, AV>), dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
-                   partials, npartials, seg, seg_bytes);
+            launch((dequant_reduce_quantize_kernel<T, 4, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
+                   cs, p, partials, npartials, seg, seg_bytes, final_out);
             break;
         default:
-            launch((dequant_reduce_quantize_kernel<T, 8, AV>), dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
-                   partials, npartials, seg, seg_bytes);
+            launch((dequant_reduce_quantize_kernel<T, 8, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
+                   cs, p, partials, npartials, seg, seg_bytes, final_out);
             break;
     }
+}
+
+template <typename T, int AV>
+static void dispatch_reduce_quantize(const uint8_t* in, int64_t co, int64_t cs, int p, const uint2* partials,
+                                     int npartials, uint8_t* seg, int64_t seg_bytes, typename T::storage* final_out,
+                                     int blocks, hipStream_t s) {
+    if (p == 1) {  // one segment: the BY = 2 tree with p known (no duplicate loads)
+        if (final_out)
+            launch_reduce_quantize<T, AV, 1, true>(2, in, co, cs, p, partials, npartials, seg, seg_bytes, final_out,
+                                                   blocks, s);
+        else
+            launch_reduce_quantize<T, AV, 1, false>(2, in, co, cs, p, partials, npartials, seg, seg_bytes, nullptr,
+                                                    blocks, s);
+        return;
+    }
+    if (final_out)
+        launch_reduce_quantize<T, AV, 0, true>(reduce_by(p), in, co, cs, p, partials, npartials, seg, seg_bytes,
+                                               final_out, blocks, s);
+    else
+        launch_reduce_quantize<T, AV, 0, false>(reduce_by(p), in, co, cs, p, partials, npartials, seg, seg_bytes,
+                                                nullptr, blocks, s);
 }
 
 int fused_blocks(int64_t cs, int per_vec) {
@@ -464,18 +510,21 @@ int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void*
 template <typename T>
 int dequant_reduce_quantize_impl(const uint8_t* in, size_t in_bytes, int cs, int p, int average,
                                  const uint2* partials, int npartials, uint8_t* seg, int64_t seg_bytes, int blocks,
-                                 hipStream_t s) {
-    if (!in || !partials || !seg || cs < 0 || p <= 0 || npartials < 1) return BAGUA_ERR_INVALID_ARG;
+                                 hipStream_t s, void* final_chunk) {
+    using S = typename T::storage;
+    if (!in || !partials || (!seg && !final_chunk) || cs < 0 || p <= 0 || npartials < 1) return BAGUA_ERR_INVALID_ARG;
     if (p > kMaxFusedChunks) return BAGUA_ERR_UNSUPPORTED;
     const int64_t co = (int64_t)(in_bytes / (size_t)p);
-    if (co < (int64_t)cs + 32 || seg_bytes < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
+    if (co < (int64_t)cs + 32 || (seg && seg_bytes < (int64_t)cs + 32)) return BAGUA_ERR_INVALID_ARG;
     constexpr int N = Vec<T>::N;
-    const bool aligned = (((uintptr_t)in + 32) % N == 0) && (co % N == 0) && (((uintptr_t)seg + 32) % N == 0);
+    const bool aligned = (((uintptr_t)in + 32) % N == 0) && (co % N == 0) && (((uintptr_t)seg + 32) % N == 0) &&
+                         ((uintptr_t)final_chunk % 16 == 0);
     if (!aligned) return BAGUA_ERR_UNSUPPORTED;
+    S* const fo = static_cast<S*>(final_chunk);
     switch (avg_mode(average, p)) {
-        case 0: dispatch_reduce_quantize<T, 0>(in, co, cs, p, partials, npartials, seg, seg_bytes, blocks, s); break;
-        case 1: dispatch_reduce_quantize<T, 1>(in, co, cs, p, partials, npartials, seg, seg_bytes, blocks, s); break;
-        default: dispatch_reduce_quantize<T, 2>(in, co, cs, p, partials, npartials, seg, seg_bytes, blocks, s); break;
+        case 0: dispatch_reduce_quantize<T, 0>(in, co, cs, p, partials, npartials, seg, seg_bytes, fo, blocks, s); break;
+        case 1: dispatch_reduce_quantize<T, 1>(in, co, cs, p, partials, npartials, seg, seg_bytes, fo, blocks, s); break;
+        default: dispatch_reduce_quantize<T, 2>(in, co, cs, p, partials, npartials, seg, seg_bytes, fo, blocks, s); break;
     }
     return check_launch();
 }
@@ -484,11 +533,11 @@ template int dequant_reduce_impl<F32>(const uint8_t*, size_t, int, int, void*, i
 template int dequant_reduce_impl<F16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
 template int dequant_reduce_impl<BF16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
 template int dequant_reduce_quantize_impl<F32>(const uint8_t*, size_t, int, int, int, const uint2*, int, uint8_t*,
-                                               int64_t, int, hipStream_t);
+                                               int64_t, int, hipStream_t, void*);
 template int dequant_reduce_quantize_impl<F16>(const uint8_t*, size_t, int, int, int, const uint2*, int, uint8_t*,
-                                               int64_t, int, hipStream_t);
+                                               int64_t, int, hipStream_t, void*);
 template int dequant_reduce_quantize_impl<BF16>(const uint8_t*, size_t, int, int, int, const uint2*, int, uint8_t*,
-                                                int64_t, int, hipStream_t);
+                                                int64_t, int, hipStream_t, void*);
 
 }  // namespace bagua
 

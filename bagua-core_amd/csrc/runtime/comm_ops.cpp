@@ -120,19 +120,20 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
     if (rc) return rc;
     DeviceGuard guard(c->device_id);
     const uint64_t s = (uint64_t)(uintptr_t)c->stream;
+    // 2. (below) alltoall: slot j of recv <- rank j's segment `rank`.  One rank receives
+    // its own bytes: the MinMax steps below read them from `send` itself (their reads and
+    // the requantise's writes are separate kernels in stream order; no recv buffer), the
+    // 1-bit middle step -- one kernel that reads every segment's header while rewriting
+    // its own -- from a device copy (RCCL's single-rank copy kernel was slower: 1 GiB op
+    // 1.257 -> 1.222 ms)
+    const bool self_alias = k.p == 1 && method == BAGUA_COMPRESSION_MINMAX_UINT8;
     OpBuffer send(c), recv(c);
     TRY(send.allocate(c->device_id, k.S));
-    TRY(recv.allocate(c->device_id, k.S));
+    if (!self_alias) TRY(recv.allocate(c->device_id, k.S));
     const bagua_tensor_t sv = u8_view(send.ptr(), k.S, c->device_id);
     const bagua_tensor_t rv = u8_view(recv.ptr(), k.S, c->device_id);
     // 1. compress every chunk (target -1)
     TRY(bagua_tensor_compress_into(t, method, k.p, s, -1, &sv));
-    // 2. alltoall: slot j of recv <- rank j's segment `rank`.  One rank receives its own
-    // bytes: the MinMax steps below read them from `send` itself (their reads and the
-    // requantise's writes are separate kernels in stream order), the 1-bit middle step
-    // -- one kernel that reads every segment's header while rewriting its own -- from a
-    // device copy (RCCL's single-rank copy kernel was slower: 1 GiB op 1.257 -> 1.222 ms)
-    const bool self_alias = k.p == 1 && method == BAGUA_COMPRESSION_MINMAX_UINT8;
     if (k.p == 1 && !self_alias)
         TRY(hipMemcpyAsync(recv.as<void>(), send.as<void>(), k.S, hipMemcpyDeviceToDevice, c->stream) == hipSuccess
                 ? BAGUA_OK
@@ -155,10 +156,20 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
         // per element); BAGUA_REDUCE_RECOMPUTE=0/1 forces either way (A/B)
         const int rcm = env_int("BAGUA_REDUCE_RECOMPUTE", -1);
         const bool recompute = rcm >= 0 ? rcm != 0 : (size_t)k.p < 2 * bagua_dtype_bytes(t->dtype);
-        rc = bagua_minmax_u8_reduce_requantize(t->dtype, rbuf, k.S, (int)k.cs, k.p,
-                                               recompute ? nullptr : (void*)(uintptr_t)t->ptr, average,
-                                               send.as<uint8_t>(), k.S, k.rank, (void*)(uintptr_t)ws, ws_bytes,
-                                               (void*)(uintptr_t)s);
+        if (recompute && k.p == 1) {
+            // one rank: the own chunk is the whole tensor and nothing is gathered, so the
+            // requantise writes the final decompressed values (no step-5 launch) and not the
+            // requantised segment, which nothing would read
+            rc = bagua_minmax_u8_reduce_requantize_final(t->dtype, rbuf, k.S, (int)k.cs, k.p, (void*)(uintptr_t)t->ptr,
+                                                         average, nullptr, 0, k.rank,
+                                                         (void*)(uintptr_t)ws, ws_bytes, (void*)(uintptr_t)s);
+            if (rc == BAGUA_OK) return finish(c, BAGUA_OK);
+        } else {
+            rc = bagua_minmax_u8_reduce_requantize(t->dtype, rbuf, k.S, (int)k.cs, k.p,
+                                                   recompute ? nullptr : (void*)(uintptr_t)t->ptr, average,
+                                                   send.as<uint8_t>(), k.S, k.rank, (void*)(uintptr_t)ws, ws_bytes,
+                                                   (void*)(uintptr_t)s);
+        }
         if (rc == BAGUA_OK) done = true;
         else if (rc != BAGUA_ERR_UNSUPPORTED) return finish(c, rc);
     } else if (fused && method == BAGUA_COMPRESSION_ONEBIT && t->num_elem == t->num_elem_allocated) {

@@ -174,6 +174,18 @@ int bagua_minmax_u8_reduce_requantize(int dtype, const uint8_t* input, size_t in
                                       int num_chunks, void* tensor, int average, uint8_t* output,
                                       size_t output_bytes, int target_chunk, void* workspace,
                                       size_t workspace_bytes, bagua_stream_t stream);
+/* The same middle step (reduced chunk recomputed, never stored) with the op's
+ * final decompress of the own chunk fused in: chunk `target_chunk` of `tensor`
+ * receives the decompressed requantised values -- exactly what
+ * bagua_minmax_u8_decompress of `output` writes there.  For one rank
+ * (num_chunks = 1) this is the op's whole tail: the final decompress launch is
+ * saved.  `tensor` must be 16-B aligned at the chunk (else UNSUPPORTED).
+ * `output` may be NULL (output_bytes is then ignored): the requantised segment
+ * is not stored -- one rank gathers nothing, so nothing would read it. */
+int bagua_minmax_u8_reduce_requantize_final(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                                            int num_chunks, void* tensor, int average, uint8_t* output,
+                                            size_t output_bytes, int target_chunk, void* workspace,
+                                            size_t workspace_bytes, bagua_stream_t stream);
 
 /* Pipelined all-reduce building blocks (no reference counterpart: the same
  * kernels restricted to part of every chunk, so communication of one piece

@@ -195,12 +195,14 @@ def test_reduce_goldens(bc, goldens):
 @pytest.mark.parametrize("dtype", [F32, F16, BF16])
 @pytest.mark.parametrize("p,ragged", [(1, 0), (2, 0), (3, 0), (4, 0), (8, 0), (12, 0), (16, 0), (1, 3), (2, 5),
                                       (4, 1)])
-@pytest.mark.parametrize("store", [True, False])
+@pytest.mark.parametrize("mode", ["store", "none", "final", "final_noseg"])
 @pytest.mark.parametrize("average", [1, 0])
-def test_fused_reduce_requantize(bc, oracle_c, dtype, p, ragged, store, average):
+def test_fused_reduce_requantize(bc, oracle_c, dtype, p, ragged, mode, average):
     """bagua_minmax_u8_reduce_requantize == decompress_from + reduce_{mean,sum} + compress(target);
     with a NULL tensor (the reduced chunk recomputed, never stored) the same segment bytes and
-    nothing of the tensor written."""
+    nothing of the tensor written; _final: the same bytes, and the own chunk of the tensor holds
+    the decompressed requantised chunk (the op's final decompress there), nothing else written."""
+    store = mode == "store"
     from oracle import oracle_np as NP
     rng = np.random.default_rng(100 + p + dtype)
     cs = 40000 + 8 * p + ragged  # ragged: a tail of < one 16-B vector of elements
@@ -223,18 +225,35 @@ def test_fused_reduce_requantize(bc, oracle_c, dtype, p, ragged, store, average)
     t_d = torch.full((p * cs,), 7.0, dtype=TORCH[dtype], device="cuda")
     send_d = torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
     ws = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
-    rc = K.bagua_minmax_u8_reduce_requantize(dtype, recv_d.data_ptr(), S, cs, p, t_d.data_ptr() if store else None,
-                                             average, send_d.data_ptr(), S, r, ws.data_ptr(), ws.numel(), None)
-    if store and (r * cs * t_d.element_size()) % 16:
+    if mode.startswith("final"):
+        seg = mode == "final"
+        rc = K.bagua_minmax_u8_reduce_requantize_final(dtype, recv_d.data_ptr(), S, cs, p, t_d.data_ptr(), average,
+                                                       send_d.data_ptr() if seg else None, S if seg else 0, r,
+                                                       ws.data_ptr(), ws.numel(), None)
+    else:
+        rc = K.bagua_minmax_u8_reduce_requantize(dtype, recv_d.data_ptr(), S, cs, p,
+                                                 t_d.data_ptr() if store else None, average, send_d.data_ptr(), S, r,
+                                                 ws.data_ptr(), ws.numel(), None)
+    if mode != "none" and (r * cs * t_d.element_size()) % 16:
         assert rc == 4  # BAGUA_ERR_UNSUPPORTED: no vector path into a misaligned chunk (callers run unfused)
         return
     assert rc == 0
     got_t = to_host(t_d, dtype)
+    untouched = np.ones(p * cs, bool)
     if store:
         assert_float_bits_equal(got_t[r * cs:(r + 1) * cs], t_want[r * cs:(r + 1) * cs], dtype, "reduced chunk")
-    else:
-        assert np.all(got_t.astype(np.float32) == 7.0) if dtype != BF16 else np.all(got_t == 0x40E0)
+        untouched[r * cs:(r + 1) * cs] = False
+    elif mode.startswith("final"):
+        final_want = np.zeros(p * cs, STORAGE[dtype])
+        oracle_c.decompress_minmax_u8(send_want, p, final_want, dtype)
+        assert_float_bits_equal(got_t[r * cs:(r + 1) * cs], final_want[r * cs:(r + 1) * cs], dtype, "final chunk")
+        untouched[r * cs:(r + 1) * cs] = False
+    rest = got_t[untouched]
+    assert np.all(rest.astype(np.float32) == 7.0) if dtype != BF16 else np.all(rest == 0x40E0)
     got = send_d.cpu().numpy()
+    if mode == "final_noseg":
+        assert np.all(got == 0xA5), "no segment byte may be written without an output buffer"
+        return
     assert np.array_equal(got[r * co:(r + 1) * co], send_want[r * co:(r + 1) * co])
     other = np.ones(S, bool)
     other[r * co:(r + 1) * co] = False
