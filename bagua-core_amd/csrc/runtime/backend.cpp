@@ -20,7 +20,11 @@
 // carries a Python callback op (python_ffi_op.rs), which ctypes runs with it.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <array>
+
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <condition_variable>
 #include <cstring>
@@ -124,8 +128,8 @@ int run_op(const bagua_bucket_op_t& op, const bagua_tensor_t* flat, const char* 
 std::vector<uint64_t> take_events(BaguaBucketC* b) {
     std::lock_guard<std::mutex> g(b->mu);
     std::vector<uint64_t> ev;
-    for (auto& kv : b->events)
-        if (kv.second) ev.push_back(kv.second);
+    for (auto& kv : b->events)  // one stream wait per distinct event (tensors often share one)
+        if (kv.second && std::find(ev.begin(), ev.end(), kv.second) == ev.end()) ev.push_back(kv.second);
     b->events.clear();
     return ev;
 }
@@ -269,13 +273,31 @@ struct BaguaCommBackendC {
         return e;
     }
 
+    // BAGUA_SCHED_PROFILE=1: host time per bucket (waiting for work / execute_bucket /
+    // completion event), printed when the backend is destroyed (measurement hook)
+    bool profile = false;
+    std::vector<std::array<double, 3>> prof;
+    size_t prof_n = 0;
+    double prof_median(int k) const {
+        std::vector<double> v;
+        for (const auto& x : prof) v.push_back(x[k]);
+        if (v.empty()) return 0;
+        std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+        return v[v.size() / 2];
+    }
+
     void work() {
         (void)hipSetDevice(device);  // lib.rs:210-213
+        using clk = std::chrono::steady_clock;
+        auto us = [](clk::time_point a, clk::time_point b) {
+            return std::chrono::duration<double, std::micro>(b - a).count();
+        };
         // async: ops return once enqueued; buckets run back to back on the stream and
         // wait_pending_comm_ops waits for each bucket's completion event
         g_async_ops = async;
         for (;;) {
             std::shared_ptr<Scheduled> item;
+            const clk::time_point t_wait = clk::now();
             {
                 std::unique_lock<std::mutex> lk(mu);
                 cv_work.wait(lk, [&] { return stop || !channel.empty(); });
@@ -286,8 +308,10 @@ struct BaguaCommBackendC {
                 current = item;
                 current_start = std::chrono::steady_clock::now();
             }
+            const clk::time_point t_exec = clk::now();
             hipStream_t s = ops_stream(item->ops);
             const int rc = execute_bucket(item->bucket, item->tensors, item->events, item->ops, s);
+            const clk::time_point t_fin = clk::now();
             hipEvent_t fin = nullptr;
             if (async) {
                 // also after a failed op: its bucket's earlier work may still be queued, and
@@ -298,6 +322,10 @@ struct BaguaCommBackendC {
                 }
                 if (fin && hipEventRecord(fin, s) != hipSuccess) fin = nullptr;
                 if (!fin && s) (void)hipStreamSynchronize(s);
+            }
+            if (profile) {
+                prof.push_back({us(t_wait, t_exec), us(t_exec, t_fin), us(t_fin, clk::now())});
+                ++prof_n;
             }
             {
                 std::lock_guard<std::mutex> lk(mu);
@@ -438,6 +466,8 @@ BaguaCommBackendC* bagua_comm_backend_create(size_t schedule_channel_cap, int de
     const char* sync = std::getenv("BAGUA_BACKEND_SYNC");
     be->async = !(sync && *sync && std::atoi(sync) != 0);
     be->cap = schedule_channel_cap ? schedule_channel_cap : 1;
+    const char* prof = std::getenv("BAGUA_SCHED_PROFILE");
+    be->profile = prof && *prof && std::atoi(prof) != 0;
     be->worker = std::thread([be] { be->work(); });
     be->monitor = std::thread([be] { be->watch(); });
     return be;
@@ -457,28 +487,38 @@ void bagua_comm_backend_destroy(BaguaCommBackendC* be) {
     int n = 0;
     (void)bagua_comm_backend_wait_pending_comm_ops(be, &n);
     for (hipEvent_t e : be->spare) (void)hipEventDestroy(e);
+    if (be->profile && be->prof_n)
+        fprintf(stderr, "[bagua-core] scheduler: %zu buckets, host us per bucket (medians): waiting for work %.2f, "
+                        "execute_bucket %.2f, completion event %.2f\n", be->prof_n, be->prof_median(0),
+                be->prof_median(1), be->prof_median(2));
     delete be;
 }
 
 int bagua_comm_backend_wait_pending_comm_ops(BaguaCommBackendC* be, int* completed) {
     // lib.rs:321-337: wait for every scheduled op; the first failure is returned
     if (!be) return BAGUA_ERR_INVALID_ARG;
+    // first every scheduled bucket enqueued (the worker launches undisturbed: a
+    // hipEventSynchronize beside its launches slowed them), then every bucket's work
+    // completed (async: its completion event)
     int n = 0, rc = BAGUA_OK;
     std::unique_lock<std::mutex> lk(be->mu);
     while (!be->pending.empty()) {
-        std::shared_ptr<Scheduled> item = be->pending.front();
-        be->pending.pop_front();
-        be->cv_done.wait(lk, [&] { return item->done; });
-        if (item->finished) {  // async: the bucket's work has to complete, not just be enqueued
-            lk.unlock();
+        std::vector<std::shared_ptr<Scheduled>> items(be->pending.begin(), be->pending.end());
+        be->pending.clear();
+        for (const auto& item : items) be->cv_done.wait(lk, [&] { return item->done; });
+        lk.unlock();
+        for (const auto& item : items) {
+            if (!item->finished) continue;
             const hipError_t e = hipEventSynchronize(item->finished);
-            lk.lock();
             if (e != hipSuccess && item->status == BAGUA_OK) item->status = BAGUA_ERR_HIP;
-            be->spare.push_back(item->finished);
-            item->finished = nullptr;
         }
-        ++n;
-        if (rc == BAGUA_OK && item->status != BAGUA_OK) rc = item->status;
+        lk.lock();
+        for (const auto& item : items) {
+            if (item->finished) be->spare.push_back(item->finished);
+            item->finished = nullptr;
+            ++n;
+            if (rc == BAGUA_OK && item->status != BAGUA_OK) rc = item->status;
+        }
     }
     if (completed) *completed = n;
     return rc;

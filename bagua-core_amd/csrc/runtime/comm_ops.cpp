@@ -26,6 +26,9 @@
 #include "runtime_util.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <mutex>
 #include <cstdlib>
 #include <vector>
 
@@ -36,6 +39,39 @@ thread_local bool g_async_ops = false;
 }
 
 namespace {
+
+// BAGUA_OP_PROFILE=1: host us per centralized op, by phase, printed at exit (measurement hook)
+struct OpProfile {
+    bool on = false;
+    std::vector<double> us[5];
+    size_t n = 0;
+    std::mutex mu;
+    OpProfile() {
+        const char* e = std::getenv("BAGUA_OP_PROFILE");
+        on = e && *e == '1';
+    }
+    static double median(std::vector<double> v) {
+        if (v.empty()) return 0;
+        std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+        return v[v.size() / 2];
+    }
+    ~OpProfile() {
+        if (on && n)
+            fprintf(stderr, "[bagua-core] centralized op host us, medians (n=%zu): plan+alloc %.2f, compress %.2f, "
+                            "middle %.2f, tail %.2f, finish %.2f\n", n, median(us[0]), median(us[1]), median(us[2]),
+                    median(us[3]), median(us[4]));
+    }
+};
+OpProfile g_op_prof;
+struct OpTimer {
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    double lap() {
+        const auto now = std::chrono::steady_clock::now();
+        const double d = std::chrono::duration<double, std::micro>(now - t).count();
+        t = now;
+        return d;
+    }
+};
 
 struct Chunking {
     int p = 1, rank = 0;
@@ -115,6 +151,17 @@ class OpBuffer {
 int env_int(const char* name, long dflt);
 
 int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int average, int method, bool fused) {
+    OpTimer tm;
+    double ph[5] = {0, 0, 0, 0, 0};
+    struct Commit {
+        double* ph;
+        ~Commit() {
+            if (!g_op_prof.on) return;
+            std::lock_guard<std::mutex> g(g_op_prof.mu);
+            for (int i = 0; i < 5; ++i) g_op_prof.us[i].push_back(ph[i]);
+            ++g_op_prof.n;
+        }
+    } commit{ph};
     Chunking k;
     int rc = plan(c, t, method, &k);
     if (rc) return rc;
@@ -132,8 +179,10 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
     if (!self_alias) TRY(recv.allocate(c->device_id, k.S));
     const bagua_tensor_t sv = u8_view(send.ptr(), k.S, c->device_id);
     const bagua_tensor_t rv = u8_view(recv.ptr(), k.S, c->device_id);
+    ph[0] = tm.lap();
     // 1. compress every chunk (target -1)
     TRY(bagua_tensor_compress_into(t, method, k.p, s, -1, &sv));
+    ph[1] = tm.lap();
     if (k.p == 1 && !self_alias)
         TRY(hipMemcpyAsync(recv.as<void>(), send.as<void>(), k.S, hipMemcpyDeviceToDevice, c->stream) == hipSuccess
                 ? BAGUA_OK
@@ -163,7 +212,12 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
             rc = bagua_minmax_u8_reduce_requantize_final(t->dtype, rbuf, k.S, (int)k.cs, k.p, (void*)(uintptr_t)t->ptr,
                                                          average, nullptr, 0, k.rank,
                                                          (void*)(uintptr_t)ws, ws_bytes, (void*)(uintptr_t)s);
-            if (rc == BAGUA_OK) return finish(c, BAGUA_OK);
+            ph[2] = tm.lap();
+            if (rc == BAGUA_OK) {
+                const int r = finish(c, BAGUA_OK);
+                ph[4] = tm.lap();
+                return r;
+            }
         } else {
             rc = bagua_minmax_u8_reduce_requantize(t->dtype, rbuf, k.S, (int)k.cs, k.p,
                                                    recompute ? nullptr : (void*)(uintptr_t)t->ptr, average,

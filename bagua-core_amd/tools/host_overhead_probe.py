@@ -63,6 +63,17 @@ def main():
     res["compress_stage1_one_kernel"] = host_us(
         lambda: K.bagua_minmax_u8_compress_stage(1, 0, xp, n, n, 1, cp, S, wp, W, -1, sp))
     res["decompress_one_kernel"] = host_us(lambda: K.bagua_minmax_u8_decompress(0, cp, S, n, 1, yp, sp))
+    # the one-rank op's middle step alone (partials-only pass + requantise with the final values)
+    res["reduce_requantize_final_two_kernels"] = host_us(
+        lambda: K.bagua_minmax_u8_reduce_requantize_final(0, cp, S, n, 1, yp, 1, None, 0, 0, wp, W, sp))
+    pool_ptr = ctypes.c_uint64(0)
+    streams = (ctypes.c_uint64 * 1)(st.cuda_stream)
+
+    def pool_cycle():
+        N.C.bagua_pool_alloc(0, S, ctypes.byref(pool_ptr))
+        N.C.bagua_pool_free_after(pool_ptr.value, streams, 1)
+    res["pool_alloc_free_after"] = host_us(pool_cycle)
+    res["hip_get_device"] = host_us(lambda: N.K.bagua_last_hip_error())
     ev0, ev1 = torch.cuda.Event(), torch.cuda.Event()
     res["hipEventRecord_pair"] = host_us(lambda: (ev0.record(st), ev1.record(st)))
     uid = bagua_core.BaguaSingleCommunicatorPy.generate_nccl_unique_id_str()

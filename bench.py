@@ -807,15 +807,20 @@ def bench_backend(args, world: int, rank: int, local_rank: int):
     # order buckets become ready
     backend.register_ordered_buckets(list(reversed(buckets)))
     events = [torch.cuda.Event() for _ in range(args.buckets)]
+    # where backward's ready events are recorded: the current (default) stream, as a
+    # training loop does, or a stream of their own (BAGUA_BENCH_READY_STREAM=own, A/B)
+    ready_mode = os.environ.get("BAGUA_BENCH_READY_STREAM", "default")  # default / own / none (no ready events)
+    ready_stream = torch.cuda.Stream(device=dev) if ready_mode == "own" else None
 
     mark_s = []
 
     def iteration():
         t0 = time.perf_counter()
         for b in reversed(range(args.buckets)):
-            events[b].record()
+            if ready_mode != "none":
+                events[b].record(ready_stream)
             for t in tensors[b]:
-                backend.mark_communication_ready(t, events[b].cuda_event)
+                backend.mark_communication_ready(t, events[b].cuda_event if ready_mode != "none" else 0)
         mark_s.append(time.perf_counter() - t0)
         done = backend.wait_pending_comm_ops()
         assert done == args.buckets, done
