@@ -464,17 +464,24 @@ static int reduce_piece_impl(const uint8_t* recv, size_t recv_bytes, int cs, int
                                   static_cast<uint2*>(ws) + (size_t)piece * blocks, blocks, s, b, e);
 }
 
+// requantise elements [e0, e1) of the own chunk from every piece's partials (the
+// whole chunk: [0, cs)); the range at 0 writes the header, the one ending at cs
+// the slack
 template <typename T>
 static int requantize_pieces_impl(const void* tensor, int cs, int p, uint8_t* out, size_t out_bytes, int target,
-                                  int pieces, const void* ws, size_t ws_bytes, hipStream_t s) {
+                                  int pieces, const void* ws, size_t ws_bytes, hipStream_t s, int e0 = 0,
+                                  int e1 = -1) {
     using S = typename T::storage;
-    if (p <= 0 || cs < 0 || target < 0 || target >= p || !tensor || !out || pieces < 1) return BAGUA_ERR_INVALID_ARG;
+    if (e1 < 0) e1 = cs;
+    if (p <= 0 || cs < 0 || target < 0 || target >= p || !tensor || !out || pieces < 1 || e0 < 0 || e1 < e0 ||
+        e1 > cs)
+        return BAGUA_ERR_INVALID_ARG;
     const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     const int blocks = piece_blocks(cs, pieces, Vec<T>::N);
     if (!ws || ws_bytes < (size_t)pieces * blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
-    launch((minmax_quantize_kernel<T, true>), dim3(blocks_for(cs, Vec<T>::N, 1), 1), dim3(kBlock), 0, s,
-                       static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, (int64_t)0, (int64_t)cs, target,
+    launch((minmax_quantize_kernel<T, true>), dim3(blocks_for(e1 - e0, Vec<T>::N, 1), 1), dim3(kBlock), 0, s,
+                       static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, (int64_t)e0, (int64_t)e1, target,
                        static_cast<const uint2*>(ws), pieces * blocks, out, chunk_offset, (int64_t)out_bytes, p);
     return check_launch();
 }
@@ -653,6 +660,17 @@ int bagua_minmax_u8_requantize_pieces(int dtype, const void* tensor, int chunk_s
     hipStream_t s = static_cast<hipStream_t>(stream);
     BAGUA_DTYPE_DISPATCH(dtype, requantize_pieces_impl<T>(tensor, chunk_size, num_chunks, output, output_bytes,
                                                           target_chunk, pieces, workspace, workspace_bytes, s));
+}
+int bagua_minmax_u8_requantize_piece(int dtype, const void* tensor, int chunk_size, int num_chunks, uint8_t* output,
+                                     size_t output_bytes, int target_chunk, int pieces, int piece,
+                                     const void* workspace, size_t workspace_bytes, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (chunk_size < 0 || pieces < 1 || piece < 0 || piece >= pieces) return BAGUA_ERR_INVALID_ARG;
+    int b, e;
+    piece_range(chunk_size, pieces, piece, &b, &e);
+    if (b == e && piece > 0) return BAGUA_OK;  // empty trailing piece: its bytes were written by the others
+    BAGUA_DTYPE_DISPATCH(dtype, requantize_pieces_impl<T>(tensor, chunk_size, num_chunks, output, output_bytes,
+                                                          target_chunk, pieces, workspace, workspace_bytes, s, b, e));
 }
 #undef BAGUA_DTYPE_DISPATCH
 

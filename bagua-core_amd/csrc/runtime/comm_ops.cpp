@@ -360,12 +360,13 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
     if (pieces < 1) pieces = k.p == 1 ? 1 : auto_pieces(k.cs);  // one rank: no exchange to hide
     if (pieces == 1 || !pipeline_fits(c, t, k)) return centralized(c, t, average, BAGUA_COMPRESSION_MINMAX_UINT8, true);
     DeviceGuard guard(c->device_id);
-    if (c->ensure_side(3 * (size_t)pieces + 1)) return BAGUA_ERR_HIP;
+    if (c->ensure_side(4 * (size_t)pieces + 1)) return BAGUA_ERR_HIP;
     hipStream_t s0 = c->stream, s1 = c->side;
     hipEvent_t* quantised = c->events.data();
     hipEvent_t* exchanged = quantised + pieces;
     hipEvent_t* gathered = exchanged + pieces;
-    hipEvent_t requantised = gathered[pieces];
+    hipEvent_t* requantised_piece = gathered + pieces;
+    hipEvent_t requantised = requantised_piece[pieces];
     const int dt = t->dtype, cs = (int)k.cs, p = k.p;
     void* x = (void*)(uintptr_t)t->ptr;
     OpBuffer send(c), recv(c);
@@ -404,13 +405,17 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
         HIP2(hipStreamWaitEvent(s0, exchanged[q], 0));
         TRY2(bagua_minmax_u8_reduce_piece(dt, rb, k.S, cs, p, x, average, k.rank, pieces, q, ws, ws_bytes, s0));
     }
-    TRY2(bagua_minmax_u8_requantize_pieces(dt, x, cs, p, sb, k.S, k.rank, pieces, ws, ws_bytes, s0));
-    HIP2(hipEventRecord(requantised, s0));
+    // requantise piece by piece (each folds every piece's partials), so the allgather of
+    // piece q starts while piece q+1 is requantised
+    for (int q = 0; q < pieces; ++q) {
+        TRY2(bagua_minmax_u8_requantize_piece(dt, x, cs, p, sb, k.S, k.rank, pieces, q, ws, ws_bytes, s0));
+        HIP2(hipEventRecord(requantised_piece[q], s0));
+    }
     // 3. allgather + dequantise piece by piece
-    HIP2(hipStreamWaitEvent(s1, requantised, 0));
     for (int q = 0; q < pieces; ++q) {
         size_t lo, hi;
         piece_bytes(k, pieces, q, &lo, &hi);
+        HIP2(hipStreamWaitEvent(s1, requantised_piece[q], 0));
         TRY2(exchange_piece(c, k, sb, rb, lo, hi, false));
         HIP2(hipEventRecord(gathered[q], s1));
     }

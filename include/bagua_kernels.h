@@ -197,7 +197,9 @@ int bagua_minmax_u8_reduce_requantize_final(int dtype, const uint8_t* input, siz
  *   bagua_minmax_u8_quantize_range per piece (the range at 0 writes headers);
  *   bagua_minmax_u8_reduce_piece per piece (fused dequantise + reduce of the
  *   target chunk; min/max partials to the piece's workspace slot), then
- *   bagua_minmax_u8_requantize_pieces (folds every slot);
+ *   bagua_minmax_u8_requantize_pieces (folds every slot), or
+ *   bagua_minmax_u8_requantize_piece per piece (each folds every slot; the
+ *   allgather of piece q can start once piece q is requantised);
  *   bagua_minmax_u8_decompress_range per piece (needs the headers present). */
 int bagua_minmax_u8_piece_range(int chunk_size, int pieces, int piece, int* begin, int* end);
 size_t bagua_minmax_u8_pipeline_workspace_bytes(int chunk_size, int pieces);
@@ -214,6 +216,9 @@ int bagua_minmax_u8_reduce_piece(int dtype, const uint8_t* input, size_t input_b
 int bagua_minmax_u8_requantize_pieces(int dtype, const void* tensor, int chunk_size, int num_chunks, uint8_t* output,
                                       size_t output_bytes, int target_chunk, int pieces, const void* workspace,
                                       size_t workspace_bytes, bagua_stream_t stream);
+int bagua_minmax_u8_requantize_piece(int dtype, const void* tensor, int chunk_size, int num_chunks, uint8_t* output,
+                                     size_t output_bytes, int target_chunk, int pieces, int piece,
+                                     const void* workspace, size_t workspace_bytes, bagua_stream_t stream);
 
 /* Decentralized ring op (decentralized_low_precision_synchronous.rs:45-64,126-151)
  * as two fused passes around the MinMax quantise pass, bit-identical to the
