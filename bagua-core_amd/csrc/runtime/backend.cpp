@@ -278,13 +278,14 @@ struct BaguaCommBackendC {
     bool profile = false;
     std::vector<std::array<double, 3>> prof;
     size_t prof_n = 0;
-    double prof_median(int k) const {
+    double prof_quantile(int k, double q) const {  // over the second half of the buckets (warm)
         std::vector<double> v;
-        for (const auto& x : prof) v.push_back(x[k]);
+        for (size_t i = prof.size() / 2; i < prof.size(); ++i) v.push_back(prof[i][k]);
         if (v.empty()) return 0;
-        std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
-        return v[v.size() / 2];
+        std::sort(v.begin(), v.end());
+        return v[(size_t)(q * (double)(v.size() - 1))];
     }
+    double prof_median(int k) const { return prof_quantile(k, 0.5); }
 
     void work() {
         (void)hipSetDevice(device);  // lib.rs:210-213
@@ -488,9 +489,11 @@ void bagua_comm_backend_destroy(BaguaCommBackendC* be) {
     (void)bagua_comm_backend_wait_pending_comm_ops(be, &n);
     for (hipEvent_t e : be->spare) (void)hipEventDestroy(e);
     if (be->profile && be->prof_n)
-        fprintf(stderr, "[bagua-core] scheduler: %zu buckets, host us per bucket (medians): waiting for work %.2f, "
-                        "execute_bucket %.2f, completion event %.2f\n", be->prof_n, be->prof_median(0),
-                be->prof_median(1), be->prof_median(2));
+        fprintf(stderr, "[bagua-core] scheduler: %zu buckets, host us per bucket (p50 / p90 / max of the second "
+                        "half): waiting for work %.2f / %.2f / %.2f, execute_bucket %.2f / %.2f / %.2f, completion "
+                        "event %.2f / %.2f / %.2f\n", be->prof_n, be->prof_median(0), be->prof_quantile(0, 0.9),
+                be->prof_quantile(0, 1.0), be->prof_median(1), be->prof_quantile(1, 0.9), be->prof_quantile(1, 1.0),
+                be->prof_median(2), be->prof_quantile(2, 0.9), be->prof_quantile(2, 1.0));
     delete be;
 }
 
