@@ -260,6 +260,68 @@ def test_fused_reduce_requantize(bc, oracle_c, dtype, p, ragged, mode, average):
     assert np.all(got[other] == 0xA5), "bytes outside the target segment written"
 
 
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("p,pieces", [(1, 3), (2, 4), (4, 2), (8, 5)])
+def test_minmax_piecewise_building_blocks(bc, oracle_c, dtype, p, pieces):
+    """The pipelined op's MinMax building blocks reproduce the unpieced bytes: quantize_range over
+    every piece (after the stage-1 partials) == compress; reduce_piece + requantize_piece over every
+    piece (requantised in reverse order) == decompress + reduce_mean + compress(target);
+    decompress_range over every piece == decompress."""
+    from oracle import oracle_np as NP
+    K = bc._native.K
+    rng = np.random.default_rng(700 + p + pieces + dtype)
+    cs = 512 * 7 * pieces + 8 * p  # trailing pieces of different length, 16-B vectors throughout
+    xs = [NP.from_f32((rng.standard_normal(p * cs) * 1e-3).astype(np.float32), dtype) for _ in range(p)]
+    r = p - 1
+    comps = [oracle_c.compress_minmax_u8(x, dtype, p) for x in xs]
+    S = comps[0].size
+    co = S // p
+    ws = torch.empty(K.bagua_minmax_u8_pipeline_workspace_bytes(cs, pieces) + (1 << 20), dtype=torch.uint8,
+                     device="cuda")
+    # 1. compress, piece by piece
+    x_d = to_dev(xs[0], dtype)
+    out_d = torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
+    assert K.bagua_minmax_u8_compress_stage(5, dtype, x_d.data_ptr(), p * cs, cs, p, out_d.data_ptr(), S,
+                                            ws.data_ptr(), ws.numel(), -1, None) == 0
+    for q in range(pieces):
+        b, e = ctypes.c_int(), ctypes.c_int()
+        assert K.bagua_minmax_u8_piece_range(cs, pieces, q, ctypes.byref(b), ctypes.byref(e)) == 0
+        if q == 0 or b.value < e.value:
+            assert K.bagua_minmax_u8_quantize_range(dtype, x_d.data_ptr(), p * cs, cs, p, out_d.data_ptr(), S,
+                                                    ws.data_ptr(), ws.numel(), -1, b.value, e.value, None) == 0
+    assert np.array_equal(out_d.cpu().numpy(), comps[0])
+    # 2. middle step, piece by piece
+    recv = np.concatenate([c[r * co:(r + 1) * co] for c in comps])
+    t_want = np.zeros(p * cs, STORAGE[dtype])
+    oracle_c.decompress_minmax_u8(recv, p, t_want, dtype)
+    oracle_c.reduce_chunks(t_want, dtype, p, r, True)
+    send_want = np.zeros(S, np.uint8)
+    oracle_c.compress_minmax_u8(t_want, dtype, p, r, out=send_want)
+    recv_d = torch.from_numpy(recv).cuda()
+    t_d = torch.zeros(p * cs, dtype=TORCH[dtype], device="cuda")
+    send_d = torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
+    for q in range(pieces):
+        assert K.bagua_minmax_u8_reduce_piece(dtype, recv_d.data_ptr(), S, cs, p, t_d.data_ptr(), 1, r, pieces, q,
+                                              ws.data_ptr(), ws.numel(), None) == 0
+    for q in reversed(range(pieces)):
+        assert K.bagua_minmax_u8_requantize_piece(dtype, t_d.data_ptr(), cs, p, send_d.data_ptr(), S, r, pieces, q,
+                                                  ws.data_ptr(), ws.numel(), None) == 0
+    got = send_d.cpu().numpy()
+    assert np.array_equal(got[r * co:(r + 1) * co], send_want[r * co:(r + 1) * co])
+    assert np.all(np.delete(got, np.s_[r * co:(r + 1) * co]) == 0xA5)
+    # 3. decompress, piece by piece
+    y_d = torch.zeros(p * cs, dtype=TORCH[dtype], device="cuda")
+    for q in range(pieces):
+        b, e = ctypes.c_int(), ctypes.c_int()
+        assert K.bagua_minmax_u8_piece_range(cs, pieces, q, ctypes.byref(b), ctypes.byref(e)) == 0
+        if b.value < e.value:
+            assert K.bagua_minmax_u8_decompress_range(dtype, out_d.data_ptr(), S, cs, p, y_d.data_ptr(), b.value,
+                                                      e.value, None) == 0
+    y_want = np.zeros(p * cs, STORAGE[dtype])
+    oracle_c.decompress_minmax_u8(comps[0], p, y_want, dtype)
+    assert_float_bits_equal(to_host(y_d, dtype), y_want, dtype, "piecewise decompress")
+
+
 # ---------------------------------------------------------------- 1-bit -----
 def test_onebit_goldens(bc, goldens):
     for i in range(int(goldens["counts"][2])):
