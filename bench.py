@@ -670,6 +670,15 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
 
     t_comm = side("comm_only", comm_only)
     del cbuf, craw
+    # Bagua's default bucket size (25 MiB of fp32): the same op and the fp32 all-reduce on the
+    # first 25 MiB of the bucket, where latency, not bandwidth, sets the step
+    m = min(n, (25 << 20) // 4)
+    m -= m % (4 * 32 * world)
+    small = BaguaTensorPy(x[:m], "bucket_25mib").raw()
+    t_s = side("bucket_25mib", lambda: N.check(N.C.bagua_centralized_low_precision_pipelined(
+        comm.handle, ctypes.byref(small), 1, N.COMPRESSION_MINMAX_UINT8, user_pieces), "25 MiB op"))
+    t_sf = side("bucket_25mib_fp32", lambda: N.check(N.C.bagua_centralized_full_precision_synchronous(
+        comm.handle, ctypes.byref(small), 1), "25 MiB fp32 allreduce"))
     t_o = side("onebit", onebit_step)
     t_ou = side("onebit_unpieced", lambda: onebit_step(1))
     decentralized = None
@@ -760,6 +769,10 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
              "pieces_sweep_ms_per_step": {q: round(v * 1e3, 3) for q, v in sweep.items()} or None,
              "comm_only_ms": round(t_comm * 1e3, 3),
              "comm_only_note": "RCCL alltoall + in-place allgather of the op's S compressed bytes, nothing else",
+             "bucket_25mib": {"elements_per_rank": m, "ms_per_step": round(t_s * 1e3, 4),
+                              "fp32_ms_per_step": round(t_sf * 1e3, 4),
+                              "gib_s_total": round(world * 4.0 * m / t_s / GiB, 2),
+                              "ratio_vs_fp32": round(t_sf / t_s, 3)},
              "decentralized_bf16": decentralized,
              "onebit_allreduce": {"ms_per_step": round(t_o * 1e3, 3), "unpieced_ms_per_step": round(t_ou * 1e3, 3),
                                   "per_rank_gib_s": round(4.0 * n / t_o / GiB, 2),

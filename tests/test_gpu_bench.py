@@ -76,4 +76,7 @@ def test_allreduce_run_single_rank():
     check_cpu(d)
     assert d["config"]["config_index"] == 4 and d["config"]["parallelism"] == "dp1"
     assert d["fp32_allreduce_gib_s"] > 0 and d["onebit_allreduce"]["ms_per_step"] > 0
+    small = d["bucket_25mib"]
+    assert small["elements_per_rank"] == (25 << 20) // 4 - ((25 << 20) // 4) % 128
+    assert small["ms_per_step"] > 0 and small["fp32_ms_per_step"] > 0 and small["gib_s_total"] > 0
     assert "side_errors" not in d
