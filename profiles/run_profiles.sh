@@ -32,6 +32,9 @@ step fetch_ob 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_
   python3 bench.py --workload onebit --steps 5 --warmup 1 --no-cpu-baseline --no-cold
 step write_ob 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_ob" -o run -- \
   python3 bench.py --workload onebit --steps 5 --warmup 1 --no-cpu-baseline --no-cold
+step trace_ar1 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_ar1" -o ar1 -- \
+  python3 bench.py --workload allreduce --steps 20 --warmup 3 --no-cpu-baseline --no-decentralized \
+  > "$OUT/ar1_under_rocprof.json"
 step ring_trace 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ring_trace" -o ring -- \
   python3 bagua-core_amd/tools/ring_probe.py --steps 10
 step b_codec 200 python3 bench.py > "$OUT/b_codec.json"
