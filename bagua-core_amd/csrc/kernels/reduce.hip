@@ -372,7 +372,7 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
         }
         for (int64_t j = 32 + cs + t; j < seg_bytes; j += kBlock) seg[j] = 0;  // slack
     }
-    uint8_t* payload = seg + 32;
+    uint8_t* payload = seg ? seg + 32 : nullptr;  // FINAL without a segment writes no payload
     reduce_tiles<T, BY, AV, PF>(
         in + 32, chunk_offset, cs, p, lut,
         [&](int64_t v, const uint4& packed) {
