@@ -324,7 +324,7 @@ struct BaguaCommBackendC {
                 if (fin && hipEventRecord(fin, s) != hipSuccess) fin = nullptr;
                 if (!fin && s) (void)hipStreamSynchronize(s);
             }
-            if (profile) {
+            if (profile && prof.size() < (1u << 20)) {  // bounded: a measurement hook, not a log
                 prof.push_back({us(t_wait, t_exec), us(t_exec, t_fin), us(t_fin, clk::now())});
                 ++prof_n;
             }

@@ -158,6 +158,7 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
         ~Commit() {
             if (!g_op_prof.on) return;
             std::lock_guard<std::mutex> g(g_op_prof.mu);
+            if (g_op_prof.n >= (1u << 20)) return;  // bounded: a measurement hook, not a log
             for (int i = 0; i < 5; ++i) g_op_prof.us[i].push_back(ph[i]);
             ++g_op_prof.n;
         }
