@@ -359,6 +359,22 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
     return check_launch();
 }
 
+// Grid of a requantise whose every workgroup folds `npartials` min/max partials
+// first (the fused reduce's 2048 per piece): the fold traffic is workgroups x
+// npartials x 8 B, so the grid is capped at ~8 MB of it (never below 512, which
+// still streams at full rate).  A 1 GiB bucket's requantise pieces at p = 2 / 4 /
+// 8 (4 pieces, npartials 8192): 53.7 / 27.6 / 14.4 us per piece with the codec's
+// 8192 workgroups, 32.8 / 16.8 / 9.5 with 512 (tools/pipeline_kernels_probe.py,
+// profiles/r03_requantise_grid_ab.jsonl).  BAGUA_TUNE_RQ_BLOCKS overrides (A/B).
+static int fold_grid_target(int npartials) {
+    const int env = tune_int("BAGUA_TUNE_RQ_BLOCKS", 0);
+    if (env > 0) return env;
+    int64_t g = ((int64_t)8 << 20) / ((int64_t)(npartials > 0 ? npartials : 1) * 8);
+    if (g < 512) g = 512;
+    if (g > kQuantBlocks) g = kQuantBlocks;
+    return (int)g;
+}
+
 // defined in reduce.hip
 int fused_blocks(int64_t cs, int per_vec);
 template <typename T>
@@ -397,9 +413,10 @@ static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs
     uint2* partials = static_cast<uint2*>(ws);
     int rc = dequant_reduce_impl<T>(recv, recv_bytes, cs, p, chunk, average, partials, blocks, s, 0, cs);
     if (rc) return rc;
-    launch((minmax_quantize_kernel<T, true>), dim3(blocks_for(cs, Vec<T>::N, 1), 1), dim3(kBlock), 0, s,
-                       static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, (int64_t)0, (int64_t)cs, target,
-                       partials, blocks, out, chunk_offset, (int64_t)out_bytes, p);
+    launch((minmax_quantize_kernel<T, true>),
+           dim3(blocks_for(cs, Vec<T>::N, 1, kSubtiles, fold_grid_target(blocks)), 1), dim3(kBlock), 0, s,
+           static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, (int64_t)0, (int64_t)cs, target, partials,
+           blocks, out, chunk_offset, (int64_t)out_bytes, p);
     return check_launch();
 }
 
@@ -480,9 +497,10 @@ static int requantize_pieces_impl(const void* tensor, int cs, int p, uint8_t* ou
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     const int blocks = piece_blocks(cs, pieces, Vec<T>::N);
     if (!ws || ws_bytes < (size_t)pieces * blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
-    launch((minmax_quantize_kernel<T, true>), dim3(blocks_for(e1 - e0, Vec<T>::N, 1), 1), dim3(kBlock), 0, s,
-                       static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, (int64_t)e0, (int64_t)e1, target,
-                       static_cast<const uint2*>(ws), pieces * blocks, out, chunk_offset, (int64_t)out_bytes, p);
+    launch((minmax_quantize_kernel<T, true>),
+           dim3(blocks_for(e1 - e0, Vec<T>::N, 1, kSubtiles, fold_grid_target(pieces * blocks)), 1), dim3(kBlock), 0,
+           s, static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, (int64_t)e0, (int64_t)e1, target,
+           static_cast<const uint2*>(ws), pieces * blocks, out, chunk_offset, (int64_t)out_bytes, p);
     return check_launch();
 }
 

@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Per-rank codec kernels of the pipelined MinMax op (comm_ops.cpp centralized_pipelined)
+at p = 2, 4, 8 on a 1 GiB fp32 bucket, timed one by one on one GPU with the kernels'
+own HIP events (bagua_time_next_kernel), without the exchange: what the §6 prediction
+of the N > 1 step needs -- the prefix before the first alltoall piece (min/max pass +
+quantise of piece 0), the middle between the last alltoall and the first allgather
+piece (reduce of the last piece + requantise of piece 0), the suffix after the last
+allgather piece (dequantise of the last piece), and the total codec time per op.
+
+    python bagua-core_amd/tools/pipeline_kernels_probe.py [--pieces 4] [--reps 5]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "bagua-core_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pieces", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    from bagua_core import _native as N
+    K = N.K
+    dev = torch.device("cuda", 0)
+    n = 1 << 28
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(n, device=dev, generator=g) * 1e-3
+    st = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    out = {"bucket_bytes": 4 * n, "pieces": a.pieces}
+
+    def timed(call):
+        ts = []
+        for _ in range(a.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            e1.record(st)
+            N.check(K.bagua_time_next_kernel(e0.cuda_event, e1.cuda_event), "timing hook")
+            N.check(call(), "kernel")
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        ts.sort()
+        return ts[len(ts) // 2]
+
+    for p in (2, 4, 8):
+        cs = n // p
+        P = a.pieces
+        S = K.bagua_minmax_u8_compressed_bytes(0, cs, p)
+        wsb = max(K.bagua_minmax_u8_workspace_bytes(cs, p), K.bagua_minmax_u8_pipeline_workspace_bytes(cs, P))
+        send = torch.empty(S, dtype=torch.uint8, device=dev)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        xp, cp, wp = x.data_ptr(), send.data_ptr(), ws.data_ptr()
+        r = p - 1
+
+        def rng(q):
+            b, e = ctypes.c_int(), ctypes.c_int()
+            N.check(K.bagua_minmax_u8_piece_range(cs, P, q, ctypes.byref(b), ctypes.byref(e)), "range")
+            return b.value, e.value
+        row = {}
+        row["minmax_pass_us"] = timed(lambda: K.bagua_minmax_u8_compress_stage(5, 0, xp, n, cs, p, cp, S, wp, wsb, -1,
+                                                                                sp))
+        q_us = [timed(lambda q=q: K.bagua_minmax_u8_quantize_range(0, xp, n, cs, p, cp, S, wp, wsb, -1, *rng(q), sp))
+                for q in range(P)]
+        # the received buffer: this rank's own compressed bytes stand in for the peers'
+        r_us = [timed(lambda q=q: K.bagua_minmax_u8_reduce_piece(0, cp, S, cs, p, xp, 1, r, P, q, wp, wsb, sp))
+                for q in range(P)]
+        rq_us = [timed(lambda q=q: K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, P, q, wp, wsb, sp))
+                 for q in range(P)]
+        d_us = [timed(lambda q=q: K.bagua_minmax_u8_decompress_range(0, cp, S, cs, p, xp, *rng(q), sp))
+                for q in range(P)]
+        row.update({"quantise_piece_us": [round(v, 1) for v in q_us], "reduce_piece_us": [round(v, 1) for v in r_us],
+                    "requantise_piece_us": [round(v, 1) for v in rq_us],
+                    "dequantise_piece_us": [round(v, 1) for v in d_us]})
+        row["prefix_us"] = round(row["minmax_pass_us"] + q_us[0], 1)
+        row["middle_us"] = round(r_us[-1] + rq_us[0], 1)
+        row["suffix_us"] = round(d_us[-1], 1)
+        row["codec_total_us"] = round(row["minmax_pass_us"] + sum(q_us) + sum(r_us) + sum(rq_us) + sum(d_us), 1)
+        row["minmax_pass_us"] = round(row["minmax_pass_us"], 1)
+        out[f"p{p}"] = row
+        del send, ws
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
