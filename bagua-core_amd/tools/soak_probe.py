@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Soak: the scheduler workload (32 x 25 MiB buckets, centralized MinMax op, async) for many
+iterations, then the pipelined op and the 1-bit op at one rank; prints the device pool's
+in-use / cached / pending bytes and the stream-workspace count every N iterations, so growth
+(leaked pool blocks, events, workspaces) shows.
+
+    python bagua-core_amd/tools/soak_probe.py [--iters 400]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "bagua-core_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=400)
+    a = ap.parse_args()
+    import bagua_core
+    from bagua_core import _native as N
+    dev = torch.device("cuda", 0)
+    comm_stream = torch.cuda.Stream(device=dev)
+    uid = bagua_core.BaguaSingleCommunicatorPy.generate_nccl_unique_id_str()
+    comm = bagua_core.BaguaSingleCommunicatorPy(0, 1, 0, comm_stream.cuda_stream, uid)
+    per = (25 << 20) // 4
+    flats = [torch.randn(per, device=dev) * 1e-3 for _ in range(32)]
+    buckets, tensors = [], []
+    for b, flat in enumerate(flats):
+        ts = [bagua_core.BaguaTensorPy(v, f"b{b}.t{i}") for i, v in enumerate(flat.view(4, -1).unbind(0))]
+        bk = bagua_core.BaguaBucketPy(f"bucket{b}", ts)
+        bk.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+        buckets.append(bk)
+        tensors.append(ts)
+    backend = bagua_core.BaguaCommBackendPy(32, 0)
+    backend.register_ordered_buckets(list(reversed(buckets)))
+    ev = [torch.cuda.Event() for _ in range(32)]
+
+    def pool():
+        C = N.C
+        return {"in_use": int(C.bagua_pool_bytes_in_use(0)), "cached": int(C.bagua_pool_bytes_cached(0)),
+                "pending": int(C.bagua_pool_bytes_pending(0))}
+    t0 = time.time()
+    for it in range(a.iters):
+        for b in reversed(range(32)):
+            ev[b].record()
+            for t in tensors[b]:
+                backend.mark_communication_ready(t, ev[b].cuda_event)
+        assert backend.wait_pending_comm_ops() == 32
+        if it % max(1, a.iters // 8) == 0 or it == a.iters - 1:
+            torch.cuda.synchronize()
+            print(json.dumps({"phase": "scheduler", "iter": it, "s": round(time.time() - t0, 1), **pool()}), flush=True)
+    x = torch.randn(1 << 26, device=dev) * 1e-3
+    raw = bagua_core.BaguaTensorPy(x, "big").raw()
+    for method, name in ((N.COMPRESSION_MINMAX_UINT8, "minmax"), (N.COMPRESSION_ONEBIT, "onebit")):
+        for it in range(200):
+            N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1, method,
+                                                                  4 if it % 2 else 0), name)
+        torch.cuda.synchronize()
+        print(json.dumps({"phase": f"op_{name}", "iter": 200, **pool()}), flush=True)
+    print(json.dumps({"done": True, "s": round(time.time() - t0, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
