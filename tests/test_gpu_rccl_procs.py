@@ -183,6 +183,8 @@ def test_bench_line_multirank(tmp_path, world, fail_headline):
     assert d["n_gpus"] == world and d["value"] > 0 and d["config"]["config_index"] == 4
     assert "side_errors" not in d, d
     assert d["onebit_allreduce"]["ms_per_step"] > 0 and d["decentralized_bf16"]["ms_per_step"] > 0
+    small = d["bucket_25mib"]  # Bagua's default bucket size, op and fp32 all-reduce side by side
+    assert small["ms_per_step"] > 0 and small["fp32_ms_per_step"] > 0 and small["elements_per_rank"] % world == 0
     if fail_headline:
         assert d["headline_fallback"]["headline"].startswith("unpieced") and d["pieces"] == 1, d
     else:
