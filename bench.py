@@ -522,11 +522,20 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     torch.cuda.synchronize()
     raw = BaguaTensorPy(x, "gradient_bucket").raw()
 
-    def compressed_step(pieces=None):
-        N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
-                                                              N.COMPRESSION_MINMAX_UINT8,
-                                                              args.pieces if pieces is None else pieces),
-                "compressed allreduce")
+    headline_taper = [False]  # the autotune may pick tapered pieces (BAGUA_PIPELINE_TAPER) for the headline
+
+    def compressed_step(pieces=None, taper=None):
+        taper = headline_taper[0] if (taper is None and pieces is None) else bool(taper)
+        if taper:
+            os.environ["BAGUA_PIPELINE_TAPER"] = "1"
+        try:
+            N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
+                                                                  N.COMPRESSION_MINMAX_UINT8,
+                                                                  args.pieces if pieces is None else pieces),
+                    "compressed allreduce")
+        finally:
+            if taper:
+                os.environ.pop("BAGUA_PIPELINE_TAPER", None)
 
     def fp32_step():
         N.check(N.C.bagua_centralized_full_precision_synchronous(comm.handle, ctypes.byref(raw), 1), "fp32 allreduce")
@@ -611,8 +620,11 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             # steps at each count, the fastest max-over-ranks time wins on every rank alike
             for q in (1, 2, 4, 8, 16):
                 autotune[str(q)] = timed(lambda q=q: compressed_step(q), 2, 1)
+            for q in (4, 8):  # first and last piece half size: shorter prefix and suffix
+                autotune[f"{q}_tapered"] = timed(lambda q=q: compressed_step(q, taper=True), 2, 1)
             best = min(autotune, key=lambda q: autotune[q])
-            args.pieces = int(best)
+            args.pieces = int(best.split("_")[0])
+            headline_taper[0] = best.endswith("_tapered")
         t_c = timed(compressed_step, args.steps, args.warmup)
         err = "timed out; communicator aborted" if aborted else None
     except Exception as e:  # noqa: BLE001 - an op error on every rank alike
@@ -641,11 +653,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
 
         def tapered(q):
             # first and last piece half size (BAGUA_PIPELINE_TAPER, minmax_u8.hip piece_range)
-            os.environ["BAGUA_PIPELINE_TAPER"] = "1"
-            try:
-                compressed_step(q)
-            finally:
-                os.environ.pop("BAGUA_PIPELINE_TAPER", None)
+            compressed_step(q, taper=True)
 
         for q in (4, 5):
             sweep[f"{q}_tapered"] = side(f"pieces_{q}_tapered", lambda q=q: tapered(q))
@@ -764,6 +772,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     extra = {"per_rank_gib_s": round(per_rank, 2), "fp32_allreduce_gib_s": round(fp32, 2),
              "ratio_vs_fp32": round(per_rank / fp32, 3), "fp32_ms_per_step": round(t_f * 1e3, 3),
              "pieces": args.pieces or "auto",
+             "pieces_tapered": headline_taper[0],
              "pieces_autotune_ms_per_step": {q: round(v * 1e3, 3) for q, v in autotune.items()} or None,
              "unpieced_ms_per_step": round(t_u * 1e3, 3),
              "pieces_sweep_ms_per_step": {q: round(v * 1e3, 3) for q, v in sweep.items()} or None,

@@ -192,7 +192,9 @@ def test_bench_line_multirank(tmp_path, world, fail_headline):
         assert set(d["pieces_sweep_ms_per_step"]) == {"2", "8", "4_tapered", "5_tapered"}, d
         # the headline's piece count is chosen on the node during the warmup
         tune = d["pieces_autotune_ms_per_step"]
-        assert set(tune) == {"1", "2", "4", "8", "16"} and d["pieces"] == int(min(tune, key=tune.get)), d
+        best = min(tune, key=tune.get)
+        assert set(tune) == {"1", "2", "4", "8", "16", "4_tapered", "8_tapered"}, d
+        assert d["pieces"] == int(best.split("_")[0]) and d["pieces_tapered"] == best.endswith("_tapered"), d
         assert all(v > 0 for v in d["pieces_sweep_ms_per_step"].values()), d["pieces_sweep_ms_per_step"]
     assert d["roofline"]["frac"] > 0
     # the CPU path beside every N: rank 0 runs the op sequence for all ranks on the host cores
