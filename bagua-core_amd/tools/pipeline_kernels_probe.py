@@ -85,6 +85,32 @@ def main():
         row["minmax_pass_us"] = round(row["minmax_pass_us"], 1)
         out[f"p{p}"] = row
         del send, ws
+    # the 1-bit op (centralized_pipelined_onebit): encode pieces, finalize, fused middle
+    # step (decode p segments + reduce + re-encode + finalize), decode pieces
+    for p in (2, 4, 8):
+        cs = n // p
+        P = a.pieces
+        S = K.bagua_onebit_compressed_bytes(cs, p)
+        wsb = K.bagua_onebit_workspace_bytes(cs, p)
+        send = torch.empty(S, dtype=torch.uint8, device=dev)
+        res = torch.empty(S, dtype=torch.uint8, device=dev)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        xp, cp, rp, wp = x.data_ptr(), send.data_ptr(), res.data_ptr(), ws.data_ptr()
+
+        def trng(q):
+            b, e = ctypes.c_int(), ctypes.c_int()
+            N.check(K.bagua_onebit_piece_range(cs, P, q, ctypes.byref(b), ctypes.byref(e)), "range")
+            return b.value, e.value
+        e_us = [timed(lambda q=q: K.bagua_onebit_encode_range(0, xp, n, cs, p, cp, S, wp, wsb, *trng(q), sp))
+                for q in range(P)]
+        f_us = timed(lambda: K.bagua_onebit_finalize(wp, wsb, n, cs, p, cp, S, sp))
+        m_us = timed(lambda: K.bagua_onebit_reduce_requantize(0, cp, S, cs, p, None, 1, rp, S, p - 1, wp, wsb, sp))
+        d_us = [timed(lambda q=q: K.bagua_onebit_decompress_range(0, cp, S, cs, p, xp, *trng(q), sp))
+                for q in range(P)]
+        out[f"onebit_p{p}"] = {"encode_piece_us": [round(v, 1) for v in e_us], "finalize_us": round(f_us, 1),
+                               "middle_us": round(m_us, 1), "decode_piece_us": [round(v, 1) for v in d_us],
+                               "codec_total_us": round(sum(e_us) + f_us + m_us + sum(d_us), 1)}
+        del send, res, ws
     print(json.dumps(out), flush=True)
 
 
