@@ -30,6 +30,8 @@ core = ctypes.CDLL(CORE_PATH, mode=ctypes.RTLD_GLOBAL)
 # dtype / method / op codes (bagua_kernels.h, bagua_core.h)
 DTYPE_F32, DTYPE_F16, DTYPE_BF16, DTYPE_U8, DTYPE_I64, DTYPE_U64 = 0, 1, 2, 3, 4, 5
 COMPRESSION_NONE, COMPRESSION_MINMAX_UINT8, COMPRESSION_ONEBIT = 0, 1, 2
+# piece schedules (bagua_kernels.h): a count, optionally OR-ed with PIECES_TAPERED
+PIECES_COUNT_MASK, PIECES_TAPERED, PIECES_MULTIPATH = 0xFFFF, 0x10000, 0x20000
 OP_SUM, OP_PROD, OP_MIN, OP_MAX, OP_AVG = 0, 1, 2, 3, 10
 
 STATUS = {0: "ok", 1: "invalid argument", 2: "workspace too small", 3: "HIP launch failed",
@@ -70,6 +72,9 @@ KERNEL_SIGNATURES = {
     "bagua_status_string": (ctypes.c_char_p, [_i32]),
     "bagua_last_hip_error": (_i32, []),
     "bagua_time_next_kernel": (_i32, [_vp, _vp]),
+    "bagua_time_next_kernels": (_i32, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _i32]),
+    "bagua_timed_kernels": (_i32, []),
+    "bagua_timed_kernel_name": (_i32, [_i32, ctypes.c_char_p, ctypes.c_size_t]),
     "bagua_minmax_u8_compressed_bytes": (_sz, [_i32, _i32, _i32]),
     "bagua_minmax_u8_workspace_bytes": (_sz, [_i32, _i32]),
     "bagua_minmax_u8_compress": (_i32, [_i32, _vp, _i32, _i32, _i32, _vp, _sz, _vp, _sz, _i32, _vp]),
@@ -237,3 +242,22 @@ def check(rc: int, what: str) -> None:
         if rc == 3:
             msg += f" (hipError {K.bagua_last_hip_error()})"
         raise BaguaNativeError(f"{what} failed: {msg}")
+
+
+def time_next_kernels(events) -> None:
+    """arm the kernel library's timing hook for len(events) launches on this thread:
+    events = [(start, stop), ...] of torch.cuda.Event(enable_timing=True), already recorded once"""
+    n = len(events)
+    st = (_vp * max(1, n))(*[a.cuda_event for a, _ in events])
+    sp = (_vp * max(1, n))(*[b.cuda_event for _, b in events])
+    check(K.bagua_time_next_kernels(st, sp, n), "time_next_kernels")
+
+
+def timed_kernel_names() -> list:
+    """names of the kernels the last time_next_kernels arming timed, in launch order"""
+    out = []
+    buf = ctypes.create_string_buffer(128)
+    for i in range(K.bagua_timed_kernels()):
+        check(K.bagua_timed_kernel_name(i, buf, 128), "timed_kernel_name")
+        out.append(buf.value.decode())
+    return out

@@ -54,7 +54,10 @@ class BaguaCommBackendPy:
         N.check(rc, "register_ordered_buckets")
         for b in self._ordered:  # the native call waited for everything scheduled
             b._release_retired()
+            b._schedulers.discard(self)
         self._ordered = list(buckets)
+        for b in self._ordered:
+            b._schedulers.add(self)
         self._names = {t.name() for b in buckets for t in b.tensors()}
 
     def mark_communication_ready(self, tensor: BaguaTensorPy, ready_cuda_event_ptr: int) -> None:
@@ -80,6 +83,10 @@ class BaguaCommBackendPy:
         if rc:
             raise RuntimeError(f"comm op failed: {N.STATUS.get(rc, rc)} ({n.value} ops waited for)")
         return n.value
+
+    def _holds(self, bucket: BaguaBucketPy) -> bool:
+        """the scheduler may still run `bucket` (it is registered here)"""
+        return any(b is bucket for b in self._ordered)
 
     def failures(self) -> list[str]:
         """ops the monitor saw running longer than 300 s"""

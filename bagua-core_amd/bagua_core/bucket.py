@@ -20,6 +20,7 @@ The dataclasses below are the Python view of the ops (ops(), print_ops()).
 from __future__ import annotations
 
 import ctypes
+import weakref
 from dataclasses import dataclass, field
 from typing import Callable, Optional
 
@@ -120,8 +121,11 @@ class BaguaBucketPy:
         # ops removed by clear_ops while a scheduled execution of this bucket may still
         # hold their native copies (callback thunks, communicator handles): kept alive
         # until the scheduler has run everything it scheduled (the reference's Arc
-        # clones, lib.rs:143-146) -- released by BaguaCommBackendPy.wait_pending_comm_ops
+        # clones, lib.rs:143-146) -- released by BaguaCommBackendPy.wait_pending_comm_ops.
+        # Only a bucket registered with a scheduler can have such executions: execute_ops
+        # has enqueued everything (and run every callback) by the time it returns.
         self._retired: list = []
+        self._schedulers = weakref.WeakSet()  # BaguaCommBackendPy instances this bucket is registered with
 
     def __del__(self):
         h = getattr(self, "_handle", None)
@@ -143,7 +147,8 @@ class BaguaBucketPy:
 
     def clear_ops(self) -> None:
         N.check(N.C.bagua_bucket_clear_ops(self._handle), "clear ops")
-        self._retired.extend(self._ops)
+        if any(b._holds(self) for b in list(self._schedulers)):
+            self._retired.extend(self._ops)
         self._ops.clear()
 
     def _release_retired(self) -> None:

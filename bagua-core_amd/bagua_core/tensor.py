@@ -99,7 +99,9 @@ class BaguaTensorPy:
             return self._raw
         t = self._torch
         n = t.numel()
-        return N.bagua_tensor_t(t.data_ptr(), n, n, _DTYPES[t.dtype][0], self._desc.device_id)
+        dev = t.device.index if t.device.type == "cuda" else -1
+        return N.bagua_tensor_t(t.data_ptr(), n, n, _DTYPES[t.dtype][0],
+                                self._desc.device_id if dev is None else dev)
 
     def _current(self) -> N.bagua_tensor_t:
         """The cached descriptor refreshed in place from the torch tensor: the
@@ -110,6 +112,11 @@ class BaguaTensorPy:
         t = self._torch
         d = self._desc
         n = t.numel()
+        dev = t.device.index
+        if t.device.type != "cuda" or (dev is not None and dev != d.device_id):
+            # the bucket's native check (the device may not change, datatypes/mod.rs:1079-1118)
+            # must see the device the storage is on, not the one cached at construction
+            d.device_id = -1 if t.device.type != "cuda" else dev
         d.ptr = t.data_ptr()
         d.num_elem = n
         d.num_elem_allocated = n

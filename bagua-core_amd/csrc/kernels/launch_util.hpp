@@ -20,16 +20,30 @@ extern thread_local int g_last_hip_error;
 // Bench instrumentation (bagua_time_next_kernel): when armed, the next kernel
 // this library launches on this thread records `start`/`stop` at its own start
 // and end (hipExtLaunchKernel), so its duration excludes dispatch overhead.
+// bagua_time_next_kernels arms up to kMaxTimed launches the same way (one event
+// pair each, in launch order) and remembers which kernel each one was.
 struct KernelTiming {
     hipEvent_t start = nullptr, stop = nullptr;
 };
-extern thread_local KernelTiming g_kernel_timing;
+constexpr int kMaxTimed = 32;
+struct KernelTimingQueue {
+    KernelTiming pairs[kMaxTimed];
+    const void* fn[kMaxTimed] = {};
+    int armed = 0, used = 0;
+};
+extern thread_local KernelTimingQueue g_kernel_timing;
+
+inline KernelTiming take_timing(const void* fn) {
+    KernelTimingQueue& q = g_kernel_timing;
+    if (q.used >= q.armed) return KernelTiming{};
+    q.fn[q.used] = fn;
+    return q.pairs[q.used++];
+}
 
 // every kernel of the library is launched through here
 template <typename F, typename... Args>
 inline void launch(F kernel, const dim3& grid, const dim3& block, uint32_t shmem, hipStream_t s, Args... args) {
-    const KernelTiming t = g_kernel_timing;
-    g_kernel_timing = KernelTiming{};
+    const KernelTiming t = take_timing(reinterpret_cast<const void*>(kernel));
     // one launch path for timed and untimed launches: hipLaunchKernel instead of the
     // Ext call when nothing is timed costs the host the same (4.6-5.2 us per launch
     // either way, profiles/r03_host_overhead_ab.jsonl)

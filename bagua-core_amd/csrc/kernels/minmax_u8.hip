@@ -426,20 +426,23 @@ static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs
 // `fused_blocks(longest piece)` min/max partials to slot k of the workspace;
 // the requantise folds all of them, which is the same min/max as one pass.
 //
-// BAGUA_PIPELINE_TAPER=1 (read per call; every piece user in the process reads
-// it alike): from 3 pieces on, the first and the last piece are half the size
-// of the others (weights 1, 2, ..., 2, 1; edges 512-aligned).  The pipelined
-// op's codec work before the first exchange (quantise piece 0) and after the
-// last one (dequantise the last piece) is then that of 2(pieces-1) pieces
-// with only `pieces` exchange groups.  Off by default; bench.py times it at
-// N > 1 beside the uniform split.
-static bool piece_taper() {
-    const char* v = getenv("BAGUA_PIPELINE_TAPER");
-    return v && v[0] == '1';
+// A piece schedule `pieces` is a count, optionally OR-ed with
+// BAGUA_PIECES_TAPERED: from 3 pieces on, the first and the last piece are then
+// half the size of the others (weights 1, 2, ..., 2, 1; edges 512-aligned).  The
+// pipelined op's codec work before the first exchange (quantise piece 0) and
+// after the last one (dequantise the last piece) is then that of 2(pieces-1)
+// pieces with only `pieces` exchange groups.  The schedule is an argument of
+// every piece function (the op reads its configuration once and passes it on),
+// so every rank and every building block of one op sees the same ranges.
+static bool piece_schedule_ok(int pieces) {
+    const int n = pieces & BAGUA_PIECES_COUNT_MASK;
+    return n >= 1 && (pieces & ~(BAGUA_PIECES_COUNT_MASK | BAGUA_PIECES_TAPERED | BAGUA_PIECES_MULTIPATH)) == 0;
 }
+static int piece_count(int pieces) { return pieces & BAGUA_PIECES_COUNT_MASK; }
 
-static void piece_range(int cs, int pieces, int k, int* b, int* e) {
-    if (pieces >= 3 && piece_taper()) {
+static void piece_range(int cs, int schedule, int k, int* b, int* e) {
+    const int pieces = piece_count(schedule);
+    if (pieces >= 3 && (schedule & BAGUA_PIECES_TAPERED)) {
         const int64_t W = 2 * (int64_t)(pieces - 1);
         auto edge = [&](int j) -> int {
             const int64_t w = j == 0 ? 0 : (j >= pieces ? W : 2 * (int64_t)j - 1);
@@ -456,11 +459,11 @@ static void piece_range(int cs, int pieces, int k, int* b, int* e) {
     *e = (int)(hi < cs ? hi : cs);
 }
 
-static int piece_blocks(int cs, int pieces, int per_vec) {
+static int piece_blocks(int cs, int schedule, int per_vec) {
     int longest = 0;
-    for (int k = 0; k < pieces; ++k) {
+    for (int k = 0; k < piece_count(schedule); ++k) {
         int b, e;
-        piece_range(cs, pieces, k, &b, &e);
+        piece_range(cs, schedule, k, &b, &e);
         if (e - b > longest) longest = e - b;
     }
     return fused_blocks(longest, per_vec);
@@ -470,10 +473,11 @@ template <typename T>
 static int reduce_piece_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, void* tensor, int average,
                              int target, int pieces, int piece, void* ws, size_t ws_bytes, hipStream_t s) {
     using S = typename T::storage;
-    if (p <= 0 || cs < 0 || target < 0 || target >= p || !tensor || pieces < 1 || piece < 0 || piece >= pieces)
+    if (p <= 0 || cs < 0 || target < 0 || target >= p || !tensor || !piece_schedule_ok(pieces) || piece < 0 ||
+        piece >= piece_count(pieces))
         return BAGUA_ERR_INVALID_ARG;
     const int blocks = piece_blocks(cs, pieces, Vec<T>::N);
-    if (!ws || ws_bytes < (size_t)pieces * blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
+    if (!ws || ws_bytes < (size_t)piece_count(pieces) * blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
     int b, e;
     piece_range(cs, pieces, piece, &b, &e);
     S* chunk = static_cast<S*>(tensor) + (int64_t)target * cs;
@@ -490,17 +494,18 @@ static int requantize_pieces_impl(const void* tensor, int cs, int p, uint8_t* ou
                                   int e1 = -1) {
     using S = typename T::storage;
     if (e1 < 0) e1 = cs;
-    if (p <= 0 || cs < 0 || target < 0 || target >= p || !tensor || !out || pieces < 1 || e0 < 0 || e1 < e0 ||
-        e1 > cs)
+    if (p <= 0 || cs < 0 || target < 0 || target >= p || !tensor || !out || !piece_schedule_ok(pieces) || e0 < 0 ||
+        e1 < e0 || e1 > cs)
         return BAGUA_ERR_INVALID_ARG;
     const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     const int blocks = piece_blocks(cs, pieces, Vec<T>::N);
-    if (!ws || ws_bytes < (size_t)pieces * blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
+    const int partials = piece_count(pieces) * blocks;
+    if (!ws || ws_bytes < (size_t)partials * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
     launch((minmax_quantize_kernel<T, true>),
-           dim3(blocks_for(e1 - e0, Vec<T>::N, 1, kSubtiles, fold_grid_target(pieces * blocks)), 1), dim3(kBlock), 0,
+           dim3(blocks_for(e1 - e0, Vec<T>::N, 1, kSubtiles, fold_grid_target(partials)), 1), dim3(kBlock), 0,
            s, static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, (int64_t)e0, (int64_t)e1, target,
-           static_cast<const uint2*>(ws), pieces * blocks, out, chunk_offset, (int64_t)out_bytes, p);
+           static_cast<const uint2*>(ws), partials, out, chunk_offset, (int64_t)out_bytes, p);
     return check_launch();
 }
 
@@ -636,14 +641,15 @@ int bagua_minmax_u8_reduce_requantize_final(int dtype, const uint8_t* input, siz
     return BAGUA_ERR_UNSUPPORTED
 
 int bagua_minmax_u8_piece_range(int chunk_size, int pieces, int piece, int* begin, int* end) {
-    if (chunk_size < 0 || pieces < 1 || piece < 0 || piece >= pieces || !begin || !end) return BAGUA_ERR_INVALID_ARG;
+    if (chunk_size < 0 || !piece_schedule_ok(pieces) || piece < 0 || piece >= piece_count(pieces) || !begin || !end)
+        return BAGUA_ERR_INVALID_ARG;
     piece_range(chunk_size, pieces, piece, begin, end);
     return BAGUA_OK;
 }
 
 size_t bagua_minmax_u8_pipeline_workspace_bytes(int chunk_size, int pieces) {
-    if (chunk_size < 0 || pieces < 1) return 0;
-    return (size_t)pieces * (size_t)piece_blocks(chunk_size, pieces, 4) * sizeof(uint2) + 256;
+    if (chunk_size < 0 || !piece_schedule_ok(pieces)) return 0;
+    return (size_t)piece_count(pieces) * (size_t)piece_blocks(chunk_size, pieces, 4) * sizeof(uint2) + 256;
 }
 
 int bagua_minmax_u8_quantize_range(int dtype, const void* input, int input_num_element, int chunk_size,
@@ -683,7 +689,8 @@ int bagua_minmax_u8_requantize_piece(int dtype, const void* tensor, int chunk_si
                                      size_t output_bytes, int target_chunk, int pieces, int piece,
                                      const void* workspace, size_t workspace_bytes, bagua_stream_t stream) {
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (chunk_size < 0 || pieces < 1 || piece < 0 || piece >= pieces) return BAGUA_ERR_INVALID_ARG;
+    if (chunk_size < 0 || !piece_schedule_ok(pieces) || piece < 0 || piece >= piece_count(pieces))
+        return BAGUA_ERR_INVALID_ARG;
     int b, e;
     piece_range(chunk_size, pieces, piece, &b, &e);
     if (b == e && piece > 0) return BAGUA_OK;  // empty trailing piece: its bytes were written by the others

@@ -198,8 +198,8 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
     // compresses num_elements(), datatypes/mod.rs:339): other tensors run unfused
     if (fused && method == BAGUA_COMPRESSION_MINMAX_UINT8 && t->num_elem == t->num_elem_allocated) {
         const size_t ws_bytes = bagua_minmax_u8_workspace_bytes((int)k.cs, k.p);
-        const uint64_t ws = stream_workspace(c->device_id, s, ws_bytes);
-        if (!ws) return finish(c, BAGUA_ERR_OOM);
+        uint64_t ws = 0;
+        if ((rc = stream_workspace(c->device_id, s, ws_bytes, &ws)) != BAGUA_OK) return finish(c, rc);
         // the reduced chunk is dead (step 5's decompress rewrites every element): below
         // p = 2*sizeof(T) recomputing it from the p received segments moves fewer bytes
         // than storing it and reading it back (p*cs vs 2*cs*sizeof(T); p = 1: 10 -> 3 bytes
@@ -229,8 +229,8 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
         else if (rc != BAGUA_ERR_UNSUPPORTED) return finish(c, rc);
     } else if (fused && method == BAGUA_COMPRESSION_ONEBIT && t->num_elem == t->num_elem_allocated) {
         const size_t ws_bytes = bagua_onebit_workspace_bytes((int)k.cs, 1);
-        const uint64_t ws = stream_workspace(c->device_id, s, ws_bytes);
-        if (!ws) return finish(c, BAGUA_ERR_OOM);
+        uint64_t ws = 0;
+        if ((rc = stream_workspace(c->device_id, s, ws_bytes, &ws)) != BAGUA_OK) return finish(c, rc);
         // the reduced chunk is not stored: step 5's decompress rewrites every element
         rc = bagua_onebit_reduce_requantize(t->dtype, recv.as<uint8_t>(), k.S, (int)k.cs, k.p,
                                             nullptr, average, send.as<uint8_t>(), k.S, k.rank,
@@ -278,6 +278,21 @@ int auto_pieces(size_t payload_bytes) {
     return k < 1 ? 1 : (int)k;
 }
 
+// The op's piece schedule (bagua_kernels.h: a count, optionally OR-ed with
+// BAGUA_PIECES_TAPERED): the caller's, with BAGUA_PIPELINE_TAPER=1 tapering a
+// count >= 3 the caller left plain.  Read once per op, on the calling thread, and
+// passed to every building block, so all of one op's ranges agree.
+int op_schedule(int count, int caller) {
+    int sched = count | (caller & BAGUA_PIECES_TAPERED);
+    if (count >= 3 && !(sched & BAGUA_PIECES_TAPERED) && env_int("BAGUA_PIPELINE_TAPER", 0) == 1)
+        sched |= BAGUA_PIECES_TAPERED;
+    return sched;
+}
+
+bool valid_schedule(int pieces) {
+    return (pieces & ~(BAGUA_PIECES_COUNT_MASK | BAGUA_PIECES_TAPERED | BAGUA_PIECES_MULTIPATH)) == 0;
+}
+
 bool pipeline_fits(const BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, const Chunking& k) {
     const size_t esz = bagua_dtype_bytes(t->dtype);
     const size_t vec = t->dtype == BAGUA_DTYPE_F32 ? 4 : 8;  // payload bytes per 16-B vector
@@ -285,11 +300,11 @@ bool pipeline_fits(const BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
            (t->ptr + (uint64_t)k.rank * k.cs * esz) % 16 == 0 && c->t != nullptr;
 }
 
-// bytes [lo, hi) of every segment that piece q covers: the header travels with
-// piece 0, the slack with the last non-empty piece; empty pieces move nothing
-void piece_bytes(const Chunking& k, int pieces, int q, size_t* lo, size_t* hi) {
+// bytes [lo, hi) of every segment that piece q of schedule `sched` covers: the header
+// travels with piece 0, the slack with the last non-empty piece; empty pieces move nothing
+void piece_bytes(const Chunking& k, int sched, int q, size_t* lo, size_t* hi) {
     int b = 0, e = 0;
-    bagua_minmax_u8_piece_range((int)k.cs, pieces, q, &b, &e);
+    bagua_minmax_u8_piece_range((int)k.cs, sched, q, &b, &e);
     const size_t co = k.S / k.p;
     if (q > 0 && b == e) {
         *lo = *hi = 0;
@@ -356,10 +371,14 @@ int finish_both(BaguaSingleCommunicatorC* c, int rc) {
 
 int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int average, int pieces) {
     Chunking k;
+    if (!valid_schedule(pieces)) return BAGUA_ERR_INVALID_ARG;
     int rc = plan(c, t, BAGUA_COMPRESSION_MINMAX_UINT8, &k);
     if (rc) return rc;
+    const int caller = pieces;
+    pieces &= BAGUA_PIECES_COUNT_MASK;
     if (pieces < 1) pieces = k.p == 1 ? 1 : auto_pieces(k.cs);  // one rank: no exchange to hide
     if (pieces == 1 || !pipeline_fits(c, t, k)) return centralized(c, t, average, BAGUA_COMPRESSION_MINMAX_UINT8, true);
+    const int sched = op_schedule(pieces, caller);
     DeviceGuard guard(c->device_id);
     if (c->ensure_side(4 * (size_t)pieces + 1)) return BAGUA_ERR_HIP;
     hipStream_t s0 = c->stream, s1 = c->side;
@@ -376,10 +395,12 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
     uint8_t* sb = send.as<uint8_t>();
     uint8_t* rb = recv.as<uint8_t>();
     size_t ws_bytes = bagua_minmax_u8_workspace_bytes(cs, p);
-    const size_t pws = bagua_minmax_u8_pipeline_workspace_bytes(cs, pieces);
+    const size_t pws = bagua_minmax_u8_pipeline_workspace_bytes(cs, sched);
     if (pws > ws_bytes) ws_bytes = pws;
-    void* ws = (void*)(uintptr_t)stream_workspace(c->device_id, (uint64_t)(uintptr_t)s0, ws_bytes);
-    if (!ws) return finish(c, BAGUA_ERR_OOM);
+    uint64_t wsp = 0;
+    if ((rc = stream_workspace(c->device_id, (uint64_t)(uintptr_t)s0, ws_bytes, &wsp)) != BAGUA_OK)
+        return finish(c, rc);
+    void* ws = (void*)(uintptr_t)wsp;
     // the side stream starts after everything already queued on the op's stream
     HIP2(hipEventRecord(requantised, s0));
     HIP2(hipStreamWaitEvent(s1, requantised, 0));
@@ -389,14 +410,14 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
                                         sb, k.S, ws, ws_bytes, -1, s0));
     for (int q = 0; q < pieces; ++q) {
         int b, e;
-        bagua_minmax_u8_piece_range(cs, pieces, q, &b, &e);
+        bagua_minmax_u8_piece_range(cs, sched, q, &b, &e);
         if (q == 0 || b < e)
             TRY2(bagua_minmax_u8_quantize_range(dt, x, (int)t->num_elem, cs, p, sb, k.S, ws, ws_bytes, -1, b, e, s0));
         HIP2(hipEventRecord(quantised[q], s0));
     }
     for (int q = 0; q < pieces; ++q) {
         size_t lo, hi;
-        piece_bytes(k, pieces, q, &lo, &hi);
+        piece_bytes(k, sched, q, &lo, &hi);
         HIP2(hipStreamWaitEvent(s1, quantised[q], 0));
         TRY2(exchange_piece(c, k, sb, rb, lo, hi, true));
         HIP2(hipEventRecord(exchanged[q], s1));
@@ -404,25 +425,25 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
     // 2. reduce the p received versions of the own chunk piece by piece, requantise it
     for (int q = 0; q < pieces; ++q) {
         HIP2(hipStreamWaitEvent(s0, exchanged[q], 0));
-        TRY2(bagua_minmax_u8_reduce_piece(dt, rb, k.S, cs, p, x, average, k.rank, pieces, q, ws, ws_bytes, s0));
+        TRY2(bagua_minmax_u8_reduce_piece(dt, rb, k.S, cs, p, x, average, k.rank, sched, q, ws, ws_bytes, s0));
     }
     // requantise piece by piece (each folds every piece's partials), so the allgather of
     // piece q starts while piece q+1 is requantised
     for (int q = 0; q < pieces; ++q) {
-        TRY2(bagua_minmax_u8_requantize_piece(dt, x, cs, p, sb, k.S, k.rank, pieces, q, ws, ws_bytes, s0));
+        TRY2(bagua_minmax_u8_requantize_piece(dt, x, cs, p, sb, k.S, k.rank, sched, q, ws, ws_bytes, s0));
         HIP2(hipEventRecord(requantised_piece[q], s0));
     }
     // 3. allgather + dequantise piece by piece
     for (int q = 0; q < pieces; ++q) {
         size_t lo, hi;
-        piece_bytes(k, pieces, q, &lo, &hi);
+        piece_bytes(k, sched, q, &lo, &hi);
         HIP2(hipStreamWaitEvent(s1, requantised_piece[q], 0));
         TRY2(exchange_piece(c, k, sb, rb, lo, hi, false));
         HIP2(hipEventRecord(gathered[q], s1));
     }
     for (int q = 0; q < pieces; ++q) {
         int b, e;
-        bagua_minmax_u8_piece_range(cs, pieces, q, &b, &e);
+        bagua_minmax_u8_piece_range(cs, sched, q, &b, &e);
         HIP2(hipStreamWaitEvent(s0, gathered[q], 0));
         if (b < e) TRY2(bagua_minmax_u8_decompress_range(dt, sb, k.S, cs, p, x, b, e, s0));
     }
@@ -440,8 +461,10 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
 //   side  :    A0 A1 .. Ak+hdr   G0+hdr G1 .. Gk
 int centralized_pipelined_onebit(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int average, int pieces) {
     Chunking k;
+    if (!valid_schedule(pieces)) return BAGUA_ERR_INVALID_ARG;
     int rc = plan(c, t, BAGUA_COMPRESSION_ONEBIT, &k);
     if (rc) return rc;
+    pieces &= BAGUA_PIECES_COUNT_MASK;  // 1-bit pieces are tile ranges: no tapered schedule
     if (pieces < 1) pieces = k.p == 1 ? 1 : auto_pieces(k.cs / 8);  // sign bits per chunk
     if (pieces == 1 || k.p > 16 || t->num_elem != t->num_elem_allocated || k.cs > 0x7fffffffULL)
         return centralized(c, t, average, BAGUA_COMPRESSION_ONEBIT, true);
@@ -459,8 +482,10 @@ int centralized_pipelined_onebit(BaguaSingleCommunicatorC* c, const bagua_tensor
     uint8_t* sb = send.as<uint8_t>();
     uint8_t* rb = recv.as<uint8_t>();
     const size_t ws_bytes = bagua_onebit_workspace_bytes(cs, p);
-    void* ws = (void*)(uintptr_t)stream_workspace(c->device_id, (uint64_t)(uintptr_t)s0, ws_bytes);
-    if (!ws) return finish(c, BAGUA_ERR_OOM);
+    uint64_t wsp = 0;
+    if ((rc = stream_workspace(c->device_id, (uint64_t)(uintptr_t)s0, ws_bytes, &wsp)) != BAGUA_OK)
+        return finish(c, rc);
+    void* ws = (void*)(uintptr_t)wsp;
     HIP2(hipEventRecord(requantised, s0));
     HIP2(hipStreamWaitEvent(s1, requantised, 0));
     // 1. encode piece by piece (bits + partials of every chunk), headers last
@@ -521,6 +546,7 @@ constexpr int kRingMinMultipath = 6;
 
 struct RingPlan {
     int p = 1, r = 0, pieces = 1, groups = 1;
+    int sched = 1;  // piece schedule (count + BAGUA_PIECES_TAPERED)
     bool mp = false;
     Chunking k;
     size_t slot = 0;  // relay scratch bytes per slice
@@ -541,9 +567,13 @@ void ring_slices(size_t lo, size_t hi, int p, size_t* b) {
 }
 
 int ring_plan(int nranks, int rank, int chunk_size, int pieces, bool multipath, RingPlan* P) {
-    if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks || chunk_size < 0 || pieces < 1) return BAGUA_ERR_INVALID_ARG;
+    if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks || chunk_size < 0 || !valid_schedule(pieces) ||
+        (pieces & BAGUA_PIECES_COUNT_MASK) < 1)
+        return BAGUA_ERR_INVALID_ARG;
     P->p = nranks;
     P->r = rank;
+    P->sched = pieces;
+    pieces &= BAGUA_PIECES_COUNT_MASK;
     P->pieces = pieces;
     P->mp = multipath && nranks >= kRingMinMultipath;
     P->groups = pieces + (P->mp ? 1 : 0);
@@ -555,7 +585,7 @@ int ring_plan(int nranks, int rank, int chunk_size, int pieces, bool multipath, 
         size_t b[65];
         for (int q = 0; q < pieces; ++q) {
             size_t lo, hi;
-            piece_bytes(P->k, pieces, q, &lo, &hi);
+            piece_bytes(P->k, P->sched, q, &lo, &hi);
             if (hi <= lo) continue;
             ring_slices(lo, hi, nranks, b);
             for (int i = 3; i < nranks; ++i)
@@ -585,7 +615,7 @@ std::vector<bagua_p2p_op_t> ring_ops(const RingPlan& P, int g) {
     size_t b[65];
     if (g < P.pieces) {
         size_t lo, hi;
-        piece_bytes(P.k, P.pieces, g, &lo, &hi);
+        piece_bytes(P.k, P.sched, g, &lo, &hi);
         if (hi > lo) {
             const size_t dhi = P.mp ? (ring_slices(lo, hi, p, b), b[3]) : hi;
             // flow 0: towards the right peer (lands in its left buffer); flow 1: towards the left peer
@@ -607,7 +637,7 @@ std::vector<bagua_p2p_op_t> ring_ops(const RingPlan& P, int g) {
     if (P.mp && g > 0) {
         const int q = g - 1;
         size_t lo, hi;
-        piece_bytes(P.k, P.pieces, q, &lo, &hi);
+        piece_bytes(P.k, P.sched, q, &lo, &hi);
         if (hi > lo) {
             ring_slices(lo, hi, p, b);
             for (int i = 3; i < p; ++i) {
@@ -659,7 +689,8 @@ int ring_exchange_group(BaguaSingleCommunicatorC* c, const RingPlan& P, int g, u
     return rc ? rc : rc_end;
 }
 
-// Opt-in (BAGUA_RING_MULTIPATH=1): the only timing so far is RCCL's socket
+// Opt-in (BAGUA_PIECES_MULTIPATH in the op's `pieces`, or BAGUA_RING_MULTIPATH=1 read
+// once per op): the only timing so far is RCCL's socket
 // transport between processes on one GPU, where multipath was 5.3x slower than
 // the direct exchange (profiles/r02_b_ar8_shared_gpu_rccl_socket.json); until an
 // xGMI node shows it faster, the default is the reference's direct exchange
@@ -698,7 +729,7 @@ int bagua_centralized_full_precision_synchronous(BaguaSingleCommunicatorC* c, co
 static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, const bagua_tensor_t* weight,
                          const bagua_tensor_t* left, const bagua_tensor_t* right, int method, bool allow_fused,
                          int pieces = 1) {
-    if (!c || !c->t || !t || !weight || !left || !right) return BAGUA_ERR_INVALID_ARG;
+    if (!c || !c->t || !t || !weight || !left || !right || !valid_schedule(pieces)) return BAGUA_ERR_INVALID_ARG;
     if (c->aborted.load()) return BAGUA_ERR_ABORTED;
     DeviceGuard guard(c->device_id);
     const uint64_t s = (uint64_t)(uintptr_t)c->stream;
@@ -728,18 +759,23 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
     if (fused) {
         // :45-64 t += L/3 + R/3 - 5W/3 (three rounded steps) with the min/max partials, then quantise
         const size_t wsb = bagua_minmax_u8_workspace_bytes(n, 1);
-        void* ws = (void*)(uintptr_t)stream_workspace(c->device_id, s, wsb);
-        if (!ws) return finish(c, BAGUA_ERR_OOM);
+        uint64_t wsp = 0;
+        if ((rc = stream_workspace(c->device_id, s, wsb, &wsp)) != BAGUA_OK) return finish(c, rc);
+        void* ws = (void*)(uintptr_t)wsp;
         rc = bagua_ring_mix_minmax(t->dtype, tp, lp, rp, wp, n, ws, wsb, sp);
         if (rc == BAGUA_OK) {
+            const int caller = pieces;
+            pieces &= BAGUA_PIECES_COUNT_MASK;
             if (pieces < 1) pieces = c->nranks == 1 ? 1 : auto_pieces((size_t)n);
-            const bool multipath = ring_multipath_enabled((int)c->nranks);
+            const int sched = op_schedule(pieces, caller);
+            const bool multipath = (caller & BAGUA_PIECES_MULTIPATH) ? (int)c->nranks >= kRingMinMultipath
+                                                                     : ring_multipath_enabled((int)c->nranks);
             if (pieces > 1 || multipath) {
                 // pipelined: quantise piece q -> exchange piece q (side stream) -> apply piece q;
                 // one header for the whole bucket, travelling with piece 0.  Multipath: the
                 // relayed slices of piece q arrive with group q + 1.
                 RingPlan plan;
-                TRY(ring_plan((int)c->nranks, (int)c->rank, n, pieces, multipath, &plan));
+                TRY(ring_plan((int)c->nranks, (int)c->rank, n, sched, multipath, &plan));
                 if (plan.k.S != S) return finish(c, BAGUA_ERR_INVALID_ARG);
                 OpBuffer relay(c);
                 if (ring_relay_bytes(plan)) TRY(relay.allocate(c->device_id, ring_relay_bytes(plan)));
@@ -756,7 +792,7 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
                 HIP2(hipStreamWaitEvent(s1, start, 0));
                 for (int q = 0; q < pieces; ++q) {
                     int b, e;
-                    bagua_minmax_u8_piece_range(n, pieces, q, &b, &e);
+                    bagua_minmax_u8_piece_range(n, sched, q, &b, &e);
                     if (q == 0 || b < e)
                         TRY2(bagua_minmax_u8_quantize_range(t->dtype, tp, n, n, 1, mb, S, ws, wsb, -1, b, e, sp));
                     HIP2(hipEventRecord(quantised[q], c->stream));
@@ -769,7 +805,7 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
                 }
                 for (int q = 0; q < pieces; ++q) {
                     int b, e;
-                    bagua_minmax_u8_piece_range(n, pieces, q, &b, &e);
+                    bagua_minmax_u8_piece_range(n, sched, q, &b, &e);
                     HIP2(hipStreamWaitEvent(c->stream, exchanged[q], 0));
                     if (b < e)
                         TRY2(bagua_ring_apply_minmax_range(t->dtype, mb, lb, rb, S, n, b, e, tp, wp, lp, rp, sp));

@@ -24,9 +24,10 @@ size_t pool_bytes(int device_id, bool cached);
 size_t pool_bytes_pending(int device_id);
 
 // Per-(device, stream) scratch reused by every launch on that stream; stream
-// order makes reuse safe without host synchronisation.
-uint64_t stream_workspace(int device_id, uint64_t stream, size_t bytes);
-uint64_t stream_workspace_generation();
+// order makes reuse safe without host synchronisation.  *out = the block;
+// BAGUA_ERR_HIP when growing it could not wait for the stream (a fault or
+// sticky error on it), BAGUA_ERR_OOM when the pool has no block.
+int stream_workspace(int device_id, uint64_t stream, size_t bytes, uint64_t* out);
 // Frees the stream's workspace after the stream has drained (communicator teardown).
 int release_stream_workspace(int device_id, uint64_t stream);
 size_t stream_workspace_count();

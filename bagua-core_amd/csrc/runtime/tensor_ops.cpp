@@ -58,34 +58,28 @@ static std::map<WorkspaceKey, std::pair<uint64_t, size_t>>& workspaces() {
     return *cache;
 }
 
-static std::atomic<uint64_t> g_ws_generation{0};
-
-// bumped whenever a stream's workspace block is replaced or freed: a HIP graph that
-// baked a workspace address (the scheduler's bucket graphs) is rebuilt when it sees
-// a newer generation than the one it was captured with
-uint64_t stream_workspace_generation() { return g_ws_generation.load(); }
-
-uint64_t stream_workspace(int device_id, uint64_t stream, size_t bytes) {
+int stream_workspace(int device_id, uint64_t stream, size_t bytes, uint64_t* out) {
+    *out = 0;
     std::lock_guard<std::mutex> g(g_ws_mu);
     auto& slot = workspaces()[workspace_key(device_id, stream)];
-    if (slot.second >= bytes && slot.first) return slot.first;
+    if (slot.second >= bytes && slot.first) {
+        *out = slot.first;
+        return BAGUA_OK;
+    }
     if (slot.first) {
-        // growing: queued work on this stream may still read the old block (under
-        // capture the sync fails and invalidates the capture: the caller runs eagerly)
-        if (hipStreamSynchronize((hipStream_t)(uintptr_t)stream) != hipSuccess) {
-            (void)hipGetLastError();
-            return 0;
-        }
+        // growing: queued work on this stream may still read the old block
+        if (hipStreamSynchronize((hipStream_t)(uintptr_t)stream) != hipSuccess) return BAGUA_ERR_HIP;
         pool_free(slot.first);
         slot = {0, 0};
-        ++g_ws_generation;
     }
     uint64_t p = 0;
     const size_t want = bytes < 65536 ? 65536 : bytes;
     // a stream's workspace outlives any op, so it never belongs to a capture arena
-    if (pool_alloc_block(device_id, want, &p) != BAGUA_OK) return 0;
+    const int rc = pool_alloc_block(device_id, want, &p);
+    if (rc != BAGUA_OK) return rc;
     slot = {p, want};
-    return p;
+    *out = p;
+    return BAGUA_OK;
 }
 
 int release_stream_workspace(int device_id, uint64_t stream) {
@@ -96,7 +90,6 @@ int release_stream_workspace(int device_id, uint64_t stream) {
     if (hipStreamSynchronize((hipStream_t)(uintptr_t)stream) != hipSuccess) return BAGUA_ERR_HIP;
     if (it->second.first) pool_free(it->second.first);
     workspaces().erase(it);
-    ++g_ws_generation;
     return BAGUA_OK;
 }
 
@@ -126,16 +119,16 @@ static int compress_into(const bagua_tensor_t* t, int method, int n_chunks, uint
     void* s = (void*)(uintptr_t)stream;
     if (method == BAGUA_COMPRESSION_MINMAX_UINT8) {
         const size_t ws_bytes = bagua_minmax_u8_workspace_bytes((int)cs, n_chunks);
-        const uint64_t ws = stream_workspace(t->device_id, stream, ws_bytes);
-        if (!ws) return BAGUA_ERR_OOM;
+        uint64_t ws = 0;
+        if ((rc = stream_workspace(t->device_id, stream, ws_bytes, &ws)) != BAGUA_OK) return rc;
         return bagua_minmax_u8_compress(t->dtype, (const void*)(uintptr_t)t->ptr, (int)t->num_elem, (int)cs, n_chunks,
                                         (uint8_t*)(uintptr_t)out_ptr, out_bytes, (void*)(uintptr_t)ws, ws_bytes, target,
                                         s);
     }
     if (method == BAGUA_COMPRESSION_ONEBIT) {
         const size_t ws_bytes = bagua_onebit_workspace_bytes((int)cs, n_chunks);
-        const uint64_t ws = stream_workspace(t->device_id, stream, ws_bytes);
-        if (!ws) return BAGUA_ERR_OOM;
+        uint64_t ws = 0;
+        if ((rc = stream_workspace(t->device_id, stream, ws_bytes, &ws)) != BAGUA_OK) return rc;
         return bagua_onebit_compress(t->dtype, (const void*)(uintptr_t)t->ptr, (int)t->num_elem, (int)cs, n_chunks,
                                      (uint8_t*)(uintptr_t)out_ptr, out_bytes, (void*)(uintptr_t)ws, ws_bytes, target, s);
     }

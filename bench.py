@@ -15,6 +15,10 @@ Metric (BASELINE.json): "GiB/s fp32 gradient encode+decode (device-resident);
       per-GPU bucket fixed).  The uncompressed fp32 RCCL all-reduce of the same
       bucket is timed beside it (fp32_allreduce_gib_s, ratio_vs_fp32).
 
+Launch: `python3 bench.py --gpus N` starts its N rank processes itself (before
+anything touches the GPU; launch_ranks), or runs as one rank under
+torch.distributed.run (RANK / WORLD_SIZE / MASTER_* set by the launcher).
+
 Every byte is produced by the gfx950 kernels through the C ABI
 (bagua-core_amd/lib/*.so).  The oracle is used ONLY for the cpu_baseline leg
 (rank 0, N = 1): the C restatement of the reference kernels timed on the
@@ -34,6 +38,72 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "bagua-core_amd"))
 sys.path.insert(0, ROOT)
+
+
+def launch_ranks(world: int, argv: list, child_cmd: list | None = None) -> int:
+    """`python3 bench.py --gpus N` without a launcher: start N rank processes of this
+    script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their
+    environment, the way torch.distributed.run sets them; rank 0's gloo store is the
+    rendezvous, as rank 0's unique id is in communicators/mod.rs:25-60), forward rank 0's
+    one JSON line, and return non-zero if any rank fails (the others are then stopped,
+    by PID).  Called before anything touches the GPU: this process never does."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = child_cmd or [sys.executable, os.path.abspath(__file__)] + list(argv)
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      stdin=subprocess.DEVNULL, text=True))
+    out = []
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0] if bad[0] > 0 else 128 - bad[0]
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.2)
+    if rc:
+        for p in procs:  # a failed rank leaves the others waiting in a collective
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        print(f"bench.py: a rank failed (exit {rc}); every rank stopped", file=sys.stderr, flush=True)
+    reader.join(timeout=30)
+    if rc == 0:
+        sys.stdout.write("".join(out))
+        sys.stdout.flush()
+    return rc
+
+
+def _maybe_launch() -> None:
+    """--gpus N > 1 with no launcher environment: become the launcher (see launch_ranks)."""
+    if "WORLD_SIZE" in os.environ:
+        return
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    known, _ = ap.parse_known_args(sys.argv[1:])
+    if known.gpus > 1:
+        sys.exit(launch_ranks(known.gpus, sys.argv[1:]))
+
+
+if __name__ == "__main__":
+    _maybe_launch()
 
 # The hardware-queue count this process inherited (the GPU box exports 4) and the
 # one HIP will actually use: both go into every line ("hw_queues").
@@ -84,6 +154,8 @@ def parse():
     ap.add_argument("--two-pass", action="store_true",
                     help="codec workload: force the two-kernel MinMax encode (BAGUA_RESIDENT=0) for A/B")
     ap.add_argument("--no-decentralized", action="store_true", help="skip the config-5 side measurement (N > 1)")
+    ap.add_argument("--no-allreduce-p1", action="store_true",
+                    help="default N = 1 line: skip the config-4 point at one rank (allreduce_p1)")
     ap.add_argument("--no-cold", action="store_true",
                     help="codec workloads: skip the two-bucket alternating side line")
     ap.add_argument("--host-buffers", type=int, default=2,
@@ -401,9 +473,45 @@ def bench_host(args):
     return value, t_ovl * 1e3, None, cfg, extra, (x[0], comp[0])
 
 
+def cgroup_cpu_quota():
+    """CPUs the cgroup lets this process use (cgroup v2 cpu.max "quota period", v1
+    cfs_quota_us / cfs_period_us), or None when unlimited / unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline_threads() -> tuple:
+    """Threads the CPU baseline runs with: min(cgroup CPU quota, affinity, OMP_NUM_THREADS
+    when the box sets one -- its stated CPU share), and the inputs of that choice."""
+    quota = cgroup_cpu_quota()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    omp_env = os.environ.get("OMP_NUM_THREADS")
+    limits = [affinity]
+    if quota is not None:
+        limits.append(max(1, int(quota)))
+    if omp_env and omp_env.strip().isdigit() and int(omp_env) > 0:
+        limits.append(int(omp_env))
+    return min(limits), {"cpu_quota": quota, "omp_num_threads_env": omp_env, "affinity_cpus": affinity}
+
+
 def host_info() -> dict:
     """The host cores the CPU baseline ran on: the machine's CPU count, this
-    process's affinity mask, the CPU model and the OpenMP threads used."""
+    process's affinity mask, the cgroup CPU quota, OMP_NUM_THREADS and the CPU model."""
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -413,11 +521,15 @@ def host_info() -> dict:
                     break
     except OSError:
         pass
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = None
-    return {"os_cpu_count": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": model}
+    threads, lim = cpu_baseline_threads()
+    return {"os_cpu_count": os.cpu_count(), "affinity_cpus": lim["affinity_cpus"], "cpu_quota": lim["cpu_quota"],
+            "omp_num_threads_env": lim["omp_num_threads_env"], "threads_rule": "min(cpu_quota, affinity, "
+            "OMP_NUM_THREADS)", "threads_allowed": threads, "cpu_model": model}
+
+
+def _oracle_threads(oracle_c) -> int:
+    """the oracle's OpenMP team = the threads the host rules allow (cpu_baseline_threads)"""
+    return oracle_c.set_num_threads(cpu_baseline_threads()[0])
 
 
 def _cpu_timed(fn, budget_s: float, max_reps: int = 100000):
@@ -439,7 +551,7 @@ def cpu_codec_baseline(args, xdev, comp_dev, onebit: bool = False):
     are compared with the CPU's (`matches_gpu_bytes`)."""
     import numpy as np
     from oracle import oracle_c
-    threads = oracle_c.num_threads()
+    threads = _oracle_threads(oracle_c)
     dcode, npdt = {torch.float32: (0, np.float32), torch.float16: (1, np.float16),
                    torch.bfloat16: (2, np.uint16)}[xdev.dtype]
     x = (xdev.view(torch.int16) if xdev.dtype == torch.bfloat16 else xdev).cpu().numpy().view(npdt)
@@ -479,7 +591,7 @@ def cpu_allreduce_baseline(args, world: int, n: int, dev, sample_elems: int = 1 
     same workload.  value = gradient bytes of all ranks / wall time."""
     import numpy as np
     from oracle import oracle_c, simulate
-    threads = oracle_c.num_threads()
+    threads = _oracle_threads(oracle_c)
     m = min(n, sample_elems)
     m -= m % world
     xs = []
@@ -494,6 +606,90 @@ def cpu_allreduce_baseline(args, world: int, n: int, dev, sample_elems: int = 1 
             "sample": f"{world} ranks x the first {4 * m >> 20} MiB of each rank's fp32 bucket (seed 0x5EED + r), "
                       f"the whole MinMax-UInt8 op sequence for all ranks x{reps} ({el:.1f} s wall, {threads} OpenMP "
                       "threads, oracle/simulate.py over oracle/bagua_oracle.c; rank 0 after the timed region)"}
+
+
+# algorithmic bytes per launch of the op's kernels at one rank (SURVEY §8(d) counting;
+# n elements of fp32, p = 1): DESIGN.md §6
+def _op_kernel_alg_bytes(name: str, n: int):
+    return {"minmax_resident_encode_kernel": 9 * n + 32, "minmax_partials_kernel": 4 * n,
+            "minmax_quantize_kernel": 5 * n + 32,
+            "dequant_reduce_kernel": n + 32,            # partials-only pass: the received payload
+            "dequant_reduce_quantize_kernel": 5 * n + 32,  # payload read + final values written (no segment)
+            "minmax_dequantize_kernel": 5 * n + 32}.get(name)
+
+
+def allreduce_p1(args, n: int = 1 << 28):
+    """Config 4 at one rank, beside the N = 1 codec headline: the same workload the N > 1
+    lines time (1 GiB fp32, the compressed centralized op,
+    centralized_low_precision_synchronous.rs:16-73, p = 1), the fp32 all-reduce of the same
+    bucket, and every kernel of the op timed by the kernel library's own events
+    (bagua_time_next_kernels), so the driver's 1 -> 8 GPU curve has a same-workload N = 1
+    point.  Steps and warmup as the headline's."""
+    from bagua_core import BaguaSingleCommunicatorPy, BaguaTensorPy
+    from bagua_core import _native as N
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    stream = torch.cuda.Stream(device=dev)
+    comm = BaguaSingleCommunicatorPy(0, 1, 0, stream.cuda_stream,
+                                     BaguaSingleCommunicatorPy.generate_nccl_unique_id_str())
+    g = torch.Generator(device=dev).manual_seed(0x5EED)
+    x = torch.randn(n, device=dev, generator=g) * 1e-3
+    torch.cuda.synchronize()
+    raw = BaguaTensorPy(x, "gradient_bucket").raw()
+
+    def op():
+        N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
+                                                              N.COMPRESSION_MINMAX_UINT8, 0), "compressed allreduce")
+
+    def fp32():
+        N.check(N.C.bagua_centralized_full_precision_synchronous(comm.handle, ctypes.byref(raw), 1), "fp32 allreduce")
+
+    def timed(fn, steps, warm):
+        for _ in range(warm):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps
+
+    t_op = timed(op, args.steps, args.warmup)
+    t_f = timed(fp32, max(3, args.steps // 2), max(1, args.warmup // 2))
+    # every kernel of the op, a few times (the op syncs its stream before returning)
+    reps, per, names = 5, {}, []
+    for _ in range(reps):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(8)]
+        for a, b in ev:
+            a.record(stream)
+            b.record(stream)
+        N.time_next_kernels(ev)
+        op()
+        names = N.timed_kernel_names()
+        N.check(N.K.bagua_time_next_kernels(None, None, 0), "disarm")
+        torch.cuda.synchronize()
+        for i, nm in enumerate(names):
+            per.setdefault(f"{i}:{nm}", []).append(ev[i][0].elapsed_time(ev[i][1]))
+    kern = {k: sum(v) / len(v) * 1e3 for k, v in per.items()}  # us
+    dom = max(kern, key=kern.get)
+    dname = dom.split(":", 1)[1]
+    alg = _op_kernel_alg_bytes(dname, n)
+    roof = None
+    if alg:
+        ach = alg / (kern[dom] * 1e-6) / 1e9
+        roof = {"bound": "hbm", "kernel": dname, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
+                "avg_launch_us": round(kern[dom], 2)}
+    res = {"config_index": 4, "workload": f"minmax_uint8_compressed_allreduce_{4 * n >> 20}MiB_fp32_per_rank",
+           "n_ranks": 1, "ms_per_step": round(t_op * 1e3, 4), "gib_s": round(4.0 * n / t_op / GiB, 2),
+           "fp32_allreduce_ms_per_step": round(t_f * 1e3, 4), "fp32_allreduce_gib_s": round(4.0 * n / t_f / GiB, 2),
+           "ratio_vs_fp32": round(t_f / t_op, 3),
+           "op_kernels_us": {k: round(v, 2) for k, v in kern.items()}, "roofline": roof,
+           "note": "the N > 1 lines' workload (--workload allreduce) at one rank; kernel times are the "
+                   "kernels' own HIP events inside the op (bagua_time_next_kernels)"}
+    del comm, x
+    torch.cuda.empty_cache()
+    return res
 
 
 # ----------------------------------------------------------------- N > 1 ------
@@ -522,20 +718,17 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     torch.cuda.synchronize()
     raw = BaguaTensorPy(x, "gradient_bucket").raw()
 
-    headline_taper = [False]  # the autotune may pick tapered pieces (BAGUA_PIPELINE_TAPER) for the headline
+    headline_taper = [False]  # the autotune may pick tapered pieces (N.PIECES_TAPERED) for the headline
 
     def compressed_step(pieces=None, taper=None):
+        # a tapered schedule goes in the op's `pieces` argument (N.PIECES_TAPERED): the
+        # process environment is never changed while ops run
         taper = headline_taper[0] if (taper is None and pieces is None) else bool(taper)
-        if taper:
-            os.environ["BAGUA_PIPELINE_TAPER"] = "1"
-        try:
-            N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
-                                                                  N.COMPRESSION_MINMAX_UINT8,
-                                                                  args.pieces if pieces is None else pieces),
-                    "compressed allreduce")
-        finally:
-            if taper:
-                os.environ.pop("BAGUA_PIPELINE_TAPER", None)
+        q = args.pieces if pieces is None else pieces
+        N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
+                                                              N.COMPRESSION_MINMAX_UINT8,
+                                                              q | (N.PIECES_TAPERED if taper else 0)),
+                "compressed allreduce")
 
     def fp32_step():
         N.check(N.C.bagua_centralized_full_precision_synchronous(comm.handle, ctypes.byref(raw), 1), "fp32 allreduce")
@@ -652,7 +845,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             sweep[str(q)] = side(f"pieces_{q}", lambda q=q: compressed_step(q))
 
         def tapered(q):
-            # first and last piece half size (BAGUA_PIPELINE_TAPER, minmax_u8.hip piece_range)
+            # first and last piece half size (N.PIECES_TAPERED, minmax_u8.hip piece_range)
             compressed_step(q, taper=True)
 
         for q in (4, 5):
@@ -698,23 +891,17 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             bufs = [(torch.randn(nb, device=dev, generator=g) * 1e-3).to(torch.bfloat16) for _ in range(4)]
             draws = [BaguaTensorPy(b, k).raw() for b, k in zip(bufs, "twlr")]
 
-            def dec_step(pieces=user_pieces):
+            def dec_step(pieces=user_pieces, multipath=False):
+                # the opt-in relayed exchange (comm_ops.cpp ring_ops: 3/p of each piece direct, the
+                # rest through the other ranks) goes in the op's `pieces` argument; the default is
+                # the reference's direct exchange
                 N.check(N.C.bagua_decentralized_low_precision_pipelined(
-                    comm.handle, *[ctypes.byref(r) for r in draws], N.COMPRESSION_MINMAX_UINT8, pieces),
-                    "decentralized")
-
-            def multipath_on(fn):
-                # opt-in relayed exchange (comm_ops.cpp ring_ops): 3/p of each piece direct,
-                # the rest through the other ranks; the default is the reference's direct one
-                os.environ["BAGUA_RING_MULTIPATH"] = "1"
-                try:
-                    fn()
-                finally:
-                    os.environ.pop("BAGUA_RING_MULTIPATH", None)
+                    comm.handle, *[ctypes.byref(r) for r in draws], N.COMPRESSION_MINMAX_UINT8,
+                    pieces | (N.PIECES_MULTIPATH if multipath else 0)), "decentralized")
 
             multipath = world >= 6  # comm_ops.cpp kRingMinMultipath
             t_d = side("decentralized", dec_step)
-            t_dm = side("decentralized_multipath", lambda: multipath_on(dec_step)) if multipath else float("nan")
+            t_dm = side("decentralized_multipath", lambda: dec_step(multipath=True)) if multipath else float("nan")
             t_du = side("decentralized_unpieced", lambda: dec_step(1))
             decentralized = {"config_index": 5, "elements_per_rank": nb, "dtype": "bf16",
                              "exchange": "direct (the reference's; multipath is opt-in)",
@@ -906,6 +1093,9 @@ def main():
         if rank == 0 and not args.no_cpu_baseline:
             cpu = cpu_codec_baseline(args, xb, cb, onebit=(workload == "onebit"))
         del xb, cb
+        if args.workload == "auto" and world == 1 and not args.no_allreduce_p1 and not args.elements:
+            # the default line: config 2 (headline) + config 4 at one rank (the 1 -> 8 GPU curve's N = 1 point)
+            extra["allreduce_p1"] = allreduce_p1(args)
         dtype = f"{args.dtype} -> u8" if workload == "codec" else f"{args.dtype} -> 1bit"
     elif workload == "host":
         value, ms, roof, cfg, extra, (xb, cb) = bench_host(args)

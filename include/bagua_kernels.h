@@ -51,6 +51,13 @@ int bagua_last_hip_error(void);
  * (hipExtLaunchKernel), so hipEventElapsedTime gives the kernel's duration
  * without dispatch overhead.  Both NULL disarms.  One-shot. */
 int bagua_time_next_kernel(void* start_event, void* stop_event);
+/* The same for the next n (<= 32) kernels this library launches on the calling
+ * thread, one event pair each in launch order (e.g. every kernel of one comm op);
+ * n = 0 disarms.  bagua_timed_kernels: how many of the armed pairs were used;
+ * bagua_timed_kernel_name: the i-th timed kernel's name ("minmax_quantize_kernel"). */
+int bagua_time_next_kernels(void* const* start_events, void* const* stop_events, int n);
+int bagua_timed_kernels(void);
+int bagua_timed_kernel_name(int i, char* buf, size_t len);
 
 /* ======================================================================== */
 /* v2 — MinMax-UInt8 codec (format: datatypes/mod.rs:669-704, K:455-500)     */
@@ -61,7 +68,10 @@ size_t bagua_minmax_u8_compressed_bytes(int dtype, int chunk_size, int num_chunk
 /* Workspace for bagua_minmax_u8_compress (replaces the cub temp-size query, K:268-310). */
 size_t bagua_minmax_u8_workspace_bytes(int chunk_size, int num_chunks);
 /* compress_{f32,f16}_to_uint8_host (K:661-676): per-chunk min/max header + uint8 payload.
- * target_chunk = -1 compresses all chunks, otherwise only chunk `target_chunk`. */
+ * target_chunk = -1 compresses all chunks, otherwise only chunk `target_chunk`.
+ * `input` must hold num_chunks*chunk_size elements: as in the reference
+ * (K:468-472, K:538-545), elements at or past input_num_element are left out of
+ * the chunk's min/max but still quantised with its parameters. */
 int bagua_minmax_u8_compress(int dtype, const void* input, int input_num_element, int chunk_size,
                              int num_chunks, uint8_t* output, size_t output_bytes, void* workspace,
                              size_t workspace_bytes, int target_chunk, bagua_stream_t stream);
@@ -200,7 +210,15 @@ int bagua_minmax_u8_reduce_requantize_final(int dtype, const uint8_t* input, siz
  *   bagua_minmax_u8_requantize_pieces (folds every slot), or
  *   bagua_minmax_u8_requantize_piece per piece (each folds every slot; the
  *   allgather of piece q can start once piece q is requantised);
- *   bagua_minmax_u8_decompress_range per piece (needs the headers present). */
+ *   bagua_minmax_u8_decompress_range per piece (needs the headers present).
+ * `pieces` is a piece schedule: the count (1..0xFFFF), optionally OR-ed with
+ * BAGUA_PIECES_TAPERED -- from 3 pieces on the first and the last piece are then
+ * half the size of the others.  Every call of one op must pass the same schedule. */
+#define BAGUA_PIECES_COUNT_MASK 0xFFFF
+#define BAGUA_PIECES_TAPERED 0x10000
+/* decentralized ring op only: the relayed (multipath) exchange from 6 ranks on
+ * (the reference's direct exchange otherwise); ignored by the piece functions */
+#define BAGUA_PIECES_MULTIPATH 0x20000
 int bagua_minmax_u8_piece_range(int chunk_size, int pieces, int piece, int* begin, int* end);
 size_t bagua_minmax_u8_pipeline_workspace_bytes(int chunk_size, int pieces);
 int bagua_minmax_u8_quantize_range(int dtype, const void* input, int input_num_element, int chunk_size,

@@ -28,6 +28,17 @@ int orc_num_threads(void) {
 #endif
 }
 
+/* the OpenMP team size of later calls (the CPU baseline: the host cores it may use) */
+int orc_set_num_threads(int n) {
+#ifdef _OPENMP
+    if (n >= 1) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
+}
+
 /* ------------------------------------------------------------------------ */
 /* scalar helpers                                                           */
 /* ------------------------------------------------------------------------ */
@@ -397,6 +408,21 @@ static float tile_tree(const float* v, int64_t count) {
     return s[0];
 }
 
+/* F over tile partials already in part[0..n), level by level in place: tile t of a
+ * level reads part[1024t, 1024t + 1024) and writes part[t], and every tile that reads
+ * part[t] (tile t / 1024) has run before it, so one ascending pass per level is exact */
+static float tree_sum_levels(float* part, int64_t n) {
+    while (n > OB_TILE) {
+        const int64_t nt = (n + OB_TILE - 1) / OB_TILE;
+        for (int64_t t = 0; t < nt; ++t) {
+            const int64_t cnt = n - t * OB_TILE;
+            part[t] = tile_tree(part + t * OB_TILE, cnt < OB_TILE ? cnt : OB_TILE);
+        }
+        n = nt;
+    }
+    return tile_tree(part, n);
+}
+
 /* F(v): one tile -> tile_tree; more -> F(tile partials).  F(empty) = 0. */
 float orc_onebit_tree_sum(const float* v, int64_t n) {
     if (n <= 0) return 0.0f;
@@ -410,9 +436,41 @@ float orc_onebit_tree_sum(const float* v, int64_t n) {
         int64_t cnt = n - t * OB_TILE;
         part[t] = tile_tree(v + t * OB_TILE, cnt < OB_TILE ? cnt : OB_TILE);
     }
-    float r = orc_onebit_tree_sum(part, nt);
+    float r = tree_sum_levels(part, nt);
     free(part);
     return r;
+}
+
+/* one tile of a chunk in one pass: its sign bits (bit = x < 0, little-endian u16
+ * field per lane) and tile_tree of its |x| (the first level of F) */
+static float onebit_tile(const void* src, int dtype, int64_t base, int64_t count, uint8_t* tile_bits) {
+    uint16_t w[64];
+    float s[64];
+    for (int lane = 0; lane < 64; ++lane) {
+        float q[4];
+        w[lane] = 0;
+        for (int sub = 0; sub < 4; ++sub) {
+            float a[4];
+            for (int e = 0; e < 4; ++e) {
+                const int64_t r = (int64_t)sub * 256 + lane * 4 + e;
+                a[e] = 0.0f;
+                if (r < count) {
+                    const float x = load_f(src, dtype, base + r);
+                    a[e] = fabsf(x);
+                    if (x < 0.0f) w[lane] |= (uint16_t)(1u << (sub * 4 + e));
+                }
+            }
+            q[sub] = (a[0] + a[1]) + (a[2] + a[3]);
+        }
+        s[lane] = (q[0] + q[1]) + (q[2] + q[3]);
+    }
+    for (int lane = 0; lane < 64; ++lane) {
+        tile_bits[2 * lane] = (uint8_t)(w[lane] & 0xff);
+        tile_bits[2 * lane + 1] = (uint8_t)(w[lane] >> 8);
+    }
+    for (int h = 32; h >= 1; h /= 2)
+        for (int l = 0; l < h; ++l) s[l] = s[l] + s[l + h];
+    return s[0];
 }
 
 int orc_compress_onebit(const void* in, int dtype, int in_num_elem, int chunk_size,
@@ -423,6 +481,9 @@ int orc_compress_onebit(const void* in, int dtype, int in_num_elem, int chunk_si
     const size_t chunk_offset = out_bytes / (size_t)num_chunks;
     const int64_t tiles = ((int64_t)chunk_size + OB_TILE - 1) / OB_TILE;
     if (chunk_offset < 32 + (size_t)tiles * OB_TILE_BYTES) return -2;
+    /* tile partials of one chunk: one small block per call (no per-chunk copy of |x|) */
+    float* part = (float*)malloc(sizeof(float) * (size_t)(tiles > 0 ? tiles : 1));
+    if (!part) return -3;
     int remaining = in_num_elem;
     for (int c = 0; c < num_chunks; ++c) {
         int n_c = remaining < chunk_size ? remaining : chunk_size;
@@ -431,41 +492,27 @@ int orc_compress_onebit(const void* in, int dtype, int in_num_elem, int chunk_si
         if (target_chunk != -1 && c != target_chunk) continue;
         const void* src = (const uint8_t*)in + (size_t)c * chunk_size * esz;
         uint8_t* seg = out + (size_t)c * chunk_offset;
-        float* absx = (float*)malloc(sizeof(float) * (size_t)(n_c > 0 ? n_c : 1));
+        uint8_t* bits = seg + 32;
+        /* elements past n_c (a partially valid chunk) are neither summed nor signed */
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static)
 #endif
-        for (int64_t j = 0; j < n_c; ++j) absx[j] = fabsf(load_f(src, dtype, j));
-        float total = orc_onebit_tree_sum(absx, n_c);
-        free(absx);
+        for (int64_t t = 0; t < tiles; ++t) {
+            const int64_t cnt = (int64_t)n_c - t * OB_TILE;
+            part[t] = onebit_tile(src, dtype, t * OB_TILE, cnt < 0 ? 0 : (cnt < OB_TILE ? cnt : OB_TILE),
+                                  bits + t * OB_TILE_BYTES);
+        }
+        const int64_t valid_tiles = ((int64_t)n_c + OB_TILE - 1) / OB_TILE;
+        float total = n_c > 0 ? tree_sum_levels(part, valid_tiles) : 0.0f;
         float scale = n_c > 0 ? total / (float)n_c : 0.0f;
         uint32_t nv = (uint32_t)n_c;
         memset(seg, 0, 32);
         memcpy(seg, &scale, 4);
         memcpy(seg + 4, &nv, 4);
-        uint8_t* bits = seg + 32;
-#ifdef _OPENMP
-#pragma omp parallel for schedule(static)
-#endif
-        for (int64_t t = 0; t < tiles; ++t) {
-            uint16_t w[64];
-            memset(w, 0, sizeof(w));
-            for (int r = 0; r < OB_TILE; ++r) {
-                int64_t j = t * OB_TILE + r;
-                if (j >= n_c) break;
-                if (load_f(src, dtype, j) < 0.0f) {
-                    int sub = r / 256, lane = (r / 4) % 64, e = r % 4;
-                    w[lane] |= (uint16_t)(1u << (sub * 4 + e));
-                }
-            }
-            for (int lane = 0; lane < 64; ++lane) { /* little-endian u16 fields */
-                bits[t * OB_TILE_BYTES + 2 * lane] = (uint8_t)(w[lane] & 0xff);
-                bits[t * OB_TILE_BYTES + 2 * lane + 1] = (uint8_t)(w[lane] >> 8);
-            }
-        }
         memset(seg + 32 + (size_t)tiles * OB_TILE_BYTES, 0,
                chunk_offset - 32 - (size_t)tiles * OB_TILE_BYTES);
     }
+    free(part);
     if (target_chunk == -1)
         memset(out + (size_t)num_chunks * chunk_offset, 0,
                out_bytes - (size_t)num_chunks * chunk_offset);

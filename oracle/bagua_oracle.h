@@ -72,6 +72,7 @@ int orc_decompress_onebit(const uint8_t* in, size_t in_bytes, int chunk_size,
 
 /* number of OpenMP threads the oracle runs with (1 when built without OpenMP) */
 int orc_num_threads(void);
+int orc_set_num_threads(int n);
 
 #ifdef __cplusplus
 }

@@ -71,6 +71,13 @@ def num_threads() -> int:
     return lib().orc_num_threads()
 
 
+def set_num_threads(n: int) -> int:
+    """OpenMP threads for later calls; returns the team size now in effect"""
+    f = lib().orc_set_num_threads
+    f.restype, f.argtypes = ctypes.c_int, [ctypes.c_int]
+    return f(int(n))
+
+
 def minmax_compressed_size(n_chunks: int, chunk_size: int, dtype: int) -> int:
     return lib().orc_minmax_compressed_size(n_chunks, chunk_size, dtype)
 

@@ -114,6 +114,34 @@ def test_piece_ranges_cover_chunk(built):
         assert pos == cs
     assert f(10, 0, 0, ctypes.byref(b), ctypes.byref(e)) != 0
     assert f(10, 2, 2, ctypes.byref(b), ctypes.byref(e)) != 0
+    assert f(10, 2 | (1 << 18), 0, ctypes.byref(b), ctypes.byref(e)) != 0  # unknown schedule bit
+
+
+def test_tapered_piece_schedule(built):
+    """BAGUA_PIECES_TAPERED in the schedule argument (no environment read): from 3 pieces on
+    the first and the last piece are about half the others, edges 512-aligned, [0, cs) tiled."""
+    from bagua_core import _native as N
+    lib = ctypes.CDLL(os.path.join(LIB, "libbagua_kernels.so"))
+    f = lib.bagua_minmax_u8_piece_range
+    f.restype = ctypes.c_int
+    ws = lib.bagua_minmax_u8_pipeline_workspace_bytes
+    ws.restype = ctypes.c_size_t
+    b, e = ctypes.c_int(), ctypes.c_int()
+    for cs, pieces in [(1 << 25, 4), (1 << 25, 8), (40000, 5), (1536, 3), (0, 4)]:
+        lens, pos = [], 0
+        for q in range(pieces):
+            assert f(cs, pieces | N.PIECES_TAPERED, q, ctypes.byref(b), ctypes.byref(e)) == 0
+            assert b.value == pos and e.value >= b.value and (b.value % 512 == 0 or b.value == cs)
+            lens.append(e.value - b.value)
+            pos = e.value
+        assert pos == cs
+        if cs >= 512 * 8 * pieces:
+            mid = lens[1]
+            assert abs(lens[0] - mid / 2) <= 512 and abs(lens[-1] - mid / 2) <= 512, lens
+        # plain and tapered schedules differ, and the workspace follows the schedule
+        assert ws(cs, pieces | N.PIECES_TAPERED) > 0
+    assert f(1 << 20, 2 | N.PIECES_TAPERED, 0, ctypes.byref(b), ctypes.byref(e)) == 0
+    assert e.value == 1 << 19  # fewer than 3 pieces: tapering does not apply
 
 
 def test_time_next_kernel_argument_check(built):

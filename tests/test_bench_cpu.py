@@ -24,7 +24,21 @@ def _args(**kw):
 def test_host_info_fields():
     h = bench.host_info()
     assert h["os_cpu_count"] >= 1 and h["affinity_cpus"] >= 1
-    assert "cpu_model" in h
+    assert "cpu_model" in h and "cpu_quota" in h and "omp_num_threads_env" in h
+    assert 1 <= h["threads_allowed"] <= h["affinity_cpus"]
+
+
+def test_cpu_baseline_threads_follow_the_host_rules(monkeypatch, oracle_c):
+    """cores = min(cgroup quota, affinity, OMP_NUM_THREADS): what the box allows, stated"""
+    monkeypatch.setattr(bench, "cgroup_cpu_quota", lambda: 2.5)
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    n, lim = bench.cpu_baseline_threads()
+    assert n == min(2, lim["affinity_cpus"]) and lim["cpu_quota"] == 2.5
+    x = torch.randn(1 << 14) * 1e-3
+    c = bench.cpu_codec_baseline(_args(), x, None)
+    assert c["cores"] == n
+    monkeypatch.undo()
+    bench._oracle_threads(oracle_c)  # later tests: the host's own rule again
 
 
 def test_cpu_codec_baseline_same_bucket(oracle_c):
@@ -48,3 +62,32 @@ def test_cpu_codec_baseline_onebit_and_bf16(oracle_c):
 def test_cpu_allreduce_baseline_all_ranks(oracle_c):
     c = bench.cpu_allreduce_baseline(_args(), 4, 1 << 14, torch.device("cpu"), sample_elems=1 << 12)
     assert c["value"] > 0 and "4 ranks" in c["sample"] and c["host"]["os_cpu_count"] >= 1
+
+
+def _fake_rank(tmp_path, body):
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys, time, json\nr = int(os.environ['RANK'])\nw = int(os.environ['WORLD_SIZE'])\n"
+                      + body)
+    return [sys.executable, str(script)]
+
+
+def test_launch_ranks_forwards_rank0_line(tmp_path, capsys):
+    """`python3 bench.py --gpus N` with no launcher: N rank processes with the
+    torch.distributed env contract, rank 0's one line forwarded, exit 0."""
+    cmd = _fake_rank(tmp_path, "assert os.environ['MASTER_ADDR'] == '127.0.0.1' and int(os.environ['MASTER_PORT'])\n"
+                               "assert os.environ['LOCAL_RANK'] == str(r)\n"
+                               "if r == 0: print(json.dumps({'n_gpus': w}))\n")
+    assert bench.launch_ranks(4, [], child_cmd=cmd) == 0
+    out = capsys.readouterr().out.strip().splitlines()
+    assert out == ['{"n_gpus": 4}']
+
+
+def test_launch_ranks_stops_every_rank_when_one_fails(tmp_path, capsys):
+    """a rank that dies leaves the others waiting in a collective: the launcher stops
+    them and fails with the dead rank's code (no line printed)."""
+    import time
+    cmd = _fake_rank(tmp_path, "if r == 1: sys.exit(3)\ntime.sleep(600)\n")
+    t0 = time.time()
+    assert bench.launch_ranks(3, [], child_cmd=cmd) == 3
+    assert time.time() - t0 < 60
+    assert capsys.readouterr().out == ""

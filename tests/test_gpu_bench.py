@@ -39,9 +39,20 @@ def check_common(d, steps, warmup):
     assert abs(r["achieved"] - r["alg_bytes_per_launch"] / (r["avg_launch_us"] * 1e-6) / 1e9) < 0.01 * r["achieved"]
 
 
-def test_default_run_is_config2_with_cpu_baseline():
-    d = run_bench("--steps", "5", "--warmup", "2", "--cpu-seconds", "0.5")
-    check_common(d, 5, 2)
+@pytest.fixture(scope="module")
+def default_line():
+    return run_bench("--steps", "20", "--warmup", "3", "--cpu-seconds", "0.5")
+
+
+@pytest.fixture(scope="module")
+def allreduce_line():
+    return run_bench("--workload", "allreduce", "--steps", "20", "--warmup", "3", "--cpu-seconds", "0.5",
+                     "--no-decentralized", timeout=200)
+
+
+def test_default_run_is_config2_with_cpu_baseline(default_line):
+    d = default_line
+    check_common(d, 20, 3)
     assert d["config"]["config_index"] == 2 and d["config"]["bucket_elements"] == 1 << 26
     # value = 256 MiB of fp32 gradient per step
     assert abs(d["value"] - 256 / 1024 / (d["ms_per_step"] * 1e-3)) < 0.01 * d["value"]
@@ -69,10 +80,9 @@ def test_onebit_run():
     assert d["cpu_baseline"]["matches_gpu_bytes"] is True
 
 
-def test_allreduce_run_single_rank():
-    d = run_bench("--workload", "allreduce", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0.5",
-                  "--no-decentralized", timeout=200)
-    check_common(d, 3, 1)
+def test_allreduce_run_single_rank(allreduce_line):
+    d = allreduce_line
+    check_common(d, 20, 3)
     check_cpu(d)
     assert d["config"]["config_index"] == 4 and d["config"]["parallelism"] == "dp1"
     assert d["fp32_allreduce_gib_s"] > 0 and d["onebit_allreduce"]["ms_per_step"] > 0
@@ -80,3 +90,19 @@ def test_allreduce_run_single_rank():
     assert small["elements_per_rank"] == (25 << 20) // 4 - ((25 << 20) // 4) % 128
     assert small["ms_per_step"] > 0 and small["fp32_ms_per_step"] > 0 and small["gib_s_total"] > 0
     assert "side_errors" not in d
+
+
+def test_default_line_carries_config4_point(default_line, allreduce_line):
+    """The default N = 1 line also times config 4 at one rank (allreduce_p1), so the driver's
+    1 -> 8 GPU curve has a same-workload N = 1 point; it agrees with --workload allreduce."""
+    a = default_line["allreduce_p1"]
+    assert a["config_index"] == 4 and a["n_ranks"] == 1
+    assert a["ms_per_step"] > 0 and a["fp32_allreduce_ms_per_step"] > 0 and a["ratio_vs_fp32"] > 0
+    assert abs(a["gib_s"] - 1.0 / (a["ms_per_step"] * 1e-3)) < 0.01 * a["gib_s"]  # 1 GiB per step
+    # every kernel of the op was timed by its own events, and the dominant one carries a roofline
+    ks = a["op_kernels_us"]
+    assert ks and all(v > 0 for v in ks.values())
+    r = a["roofline"]
+    assert r and r["kernel"] in {k.split(":", 1)[1] for k in ks} and 0 < r["frac"] < 1.2
+    ref = allreduce_line["ms_per_step"]
+    assert abs(a["ms_per_step"] - ref) <= 0.05 * ref, (a["ms_per_step"], ref)

@@ -134,8 +134,9 @@ def test_v1_abi_compress_decompress(bc, oracle_c):
 
 @pytest.mark.parametrize("dtype,p,cs,pieces,offset", [(F32, 4, 65536 + 77, 3, 0), (BF16, 3, 40000, 4, 1),
                                                       (F16, 2, 1536, 4, 0), (F32, 1, 5000, 7, 2)])
-def test_minmax_piecewise_building_blocks(bc, oracle_c, dtype, p, cs, pieces, offset):
-    """stage-1 partials + quantize_range per piece == one compress; decompress_range per piece == one decode."""
+def test_minmax_range_entry_points_misaligned(bc, oracle_c, dtype, p, cs, pieces, offset):
+    """stage-1 partials + quantize_range per piece == one compress; decompress_range per piece == one decode
+    (misaligned data pointers, F16, odd chunk sizes, ragged pieces at p = 1; K:455-500)."""
     from oracle import oracle_np as NP
     K = bc._native.K
     rng = np.random.default_rng(cs + pieces)

@@ -159,10 +159,13 @@ def test_hierarchical(tmp_path, oracle_c):
         assert np.array_equal(o["t"], want[r // per_node].view(np.uint8)), r
 
 
-@pytest.mark.parametrize("world,fail_headline", [(2, False), (8, False), (2, True)])
-def test_bench_line_multirank(tmp_path, world, fail_headline):
-    """bench.py's N > 1 line (config 4 + side lines) end to end under torch.distributed.run
-    with `world` ranks on the one GPU (BAGUA_BENCH_SHARED_GPU): the pipelined headline must
+@pytest.mark.parametrize("world,fail_headline,launcher", [(2, False, "self"), (8, False, "self"),
+                                                          (2, True, "torchrun")])
+def test_bench_line_multirank(tmp_path, world, fail_headline, launcher):
+    """bench.py's N > 1 line (config 4 + side lines) end to end with `world` ranks on the one
+    GPU (BAGUA_BENCH_SHARED_GPU), started as plain `python3 bench.py --gpus N` (bench.py
+    launches its own rank processes, launcher "self") or under torch.distributed.run: the
+    pipelined headline must
     not fall back, and the side measurements must not fail (8 ranks: the direct ring
     exchange and the opt-in multipath side line).  fail_headline: the headline's communicator
     is aborted (BAGUA_BENCH_FAIL_HEADLINE, ncclCommAbort on every rank), so the line must come
@@ -172,9 +175,14 @@ def test_bench_line_multirank(tmp_path, world, fail_headline):
     env.update({"BAGUA_BENCH_SHARED_GPU": "1", "NCCL_IB_DISABLE": "1", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
     if fail_headline:
         env["BAGUA_BENCH_FAIL_HEADLINE"] = "1"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr=127.0.0.1", f"--master-port={29517 + world + 20 * fail_headline}", os.path.join(ROOT, "bench.py"), "--gpus", str(world),
-           "--steps", "3", "--warmup", "1", "--elements", str(1 << 22), "--cpu-seconds", "1"]
+    args = ["--gpus", str(world), "--steps", "3", "--warmup", "1", "--elements", str(1 << 22), "--cpu-seconds", "1"]
+    if launcher == "self":
+        env.pop("WORLD_SIZE", None)
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr=127.0.0.1", f"--master-port={29517 + world + 20 * fail_headline}",
+               os.path.join(ROOT, "bench.py")] + args
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
