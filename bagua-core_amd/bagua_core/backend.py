@@ -88,6 +88,14 @@ class BaguaCommBackendPy:
         """the scheduler may still run `bucket` (it is registered here)"""
         return any(b is bucket for b in self._ordered)
 
+    def set_lanes(self, lanes: int) -> None:
+        """cross-bucket pipelining: bucket i runs on lane 1 + i % lanes of its communicator
+        (1 = every bucket on the communicator's stream); waits for everything scheduled"""
+        N.check(N.C.bagua_comm_backend_set_lanes(self._handle, int(lanes)), "set_lanes")
+
+    def lanes(self) -> int:
+        return int(N.C.bagua_comm_backend_lanes(self._handle))
+
     def failures(self) -> list[str]:
         """ops the monitor saw running longer than 300 s"""
         return ["comm op has not finished for 5 min"] * max(0, N.C.bagua_comm_backend_failures(self._handle))

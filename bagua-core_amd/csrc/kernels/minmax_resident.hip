@@ -54,6 +54,7 @@
 #include <chrono>
 #include <map>
 #include <mutex>
+#include <set>
 #include <thread>
 #include <utility>
 
@@ -524,6 +525,14 @@ struct ResidentDevice {
     bool warned_full = false;
 };
 static std::mutex g_res_mu;
+// streams whose compress calls never take the one-launch encode: streams that run
+// codec work concurrently with another codec stream (the scheduler's lanes), where two
+// encodes each needing every CU resident would wait on each other (bounded, but slow);
+// guarded by g_res_mu
+static std::set<hipStream_t>& resident_off_streams() {
+    static auto* s = new std::set<hipStream_t>();
+    return *s;
+}
 static uint64_t* g_res_trace = nullptr;  // bagua_minmax_u8_resident_trace
 static ResidentDevice g_res_dev[64];
 
@@ -697,6 +706,10 @@ static ResidentPlan resident_plan(const void* input, int64_t in_num_elem, int64_
     ResidentPlan pl;
     const int cfg = env_int("BAGUA_RESIDENT_CFG", kResDefaultCfg);
     if (env_int("BAGUA_RESIDENT", 1) == 0 || cfg < 0 || cfg >= kResNumCfg || p <= 0) return pl;
+    {
+        std::lock_guard<std::mutex> lk(g_res_mu);
+        if (resident_off_streams().count(s)) return pl;
+    }
     const int nact = target < 0 ? p : 1;
     const int64_t chunk_offset = out_bytes / p;
     // whole chunks only, every active chunk fully valid, large enough to pay for the exchange
@@ -885,7 +898,18 @@ template int resident_compress_impl<BF16>(const void*, int64_t, int64_t, int, ui
 }  // namespace bagua
 
 extern "C" int bagua_minmax_u8_release_stream(bagua_stream_t stream) {
+    {
+        std::lock_guard<std::mutex> lk(bagua::g_res_mu);
+        bagua::resident_off_streams().erase(static_cast<hipStream_t>(stream));
+    }
     return bagua::release_stream_slot(static_cast<hipStream_t>(stream));
+}
+
+extern "C" int bagua_minmax_u8_set_stream_resident(bagua_stream_t stream, int allowed) {
+    std::lock_guard<std::mutex> lk(bagua::g_res_mu);
+    if (allowed) bagua::resident_off_streams().erase(static_cast<hipStream_t>(stream));
+    else bagua::resident_off_streams().insert(static_cast<hipStream_t>(stream));
+    return BAGUA_OK;
 }
 
 extern "C" int bagua_minmax_u8_resident_slots_in_use(int device_id) { return bagua::resident_slots_in_use(device_id); }

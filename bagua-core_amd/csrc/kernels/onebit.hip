@@ -615,11 +615,17 @@ static int ob_decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p,
     const int64_t te = t_end < tiles ? t_end : tiles;
     if (te <= t_begin) return BAGUA_OK;
     // default-policy stores: 43 us vs 50 us with nt stores per 256 MiB decode, and the
-    // next encode (nt loads) is unaffected (profiles/r01_decode_store_ab.jsonl)
-    launch(onebit_decode_kernel<T, false>,
-           dim3(ob_blocks(te - t_begin, p, tune_int("BAGUA_TUNE_OB_DECODE_BLOCKS", kObDecodeBlocks)), p), dim3(kBlock), 0,
-           s, in, co,
-           (int64_t)cs, static_cast<S*>(out), t_begin, te);
+    // next encode (nt loads) is unaffected (profiles/r01_decode_store_ab.jsonl).
+    // BAGUA_OB_DECODE_NT=1 / 0 forces nt / default stores (A/B at sizes past the
+    // Infinity Cache, where dirty lines cannot stay behind: tools/cache_state_probe.py)
+    const int nt = tune_int("BAGUA_OB_DECODE_NT", 0);
+    const dim3 grid(ob_blocks(te - t_begin, p, tune_int("BAGUA_TUNE_OB_DECODE_BLOCKS", kObDecodeBlocks)), p);
+    if (nt == 1)
+        launch(onebit_decode_kernel<T, true>, grid, dim3(kBlock), 0, s, in, co, (int64_t)cs, static_cast<S*>(out),
+               t_begin, te);
+    else
+        launch(onebit_decode_kernel<T, false>, grid, dim3(kBlock), 0, s, in, co, (int64_t)cs, static_cast<S*>(out),
+               t_begin, te);
     return check_launch();
 }
 

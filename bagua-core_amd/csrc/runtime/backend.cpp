@@ -16,6 +16,14 @@
 //   * wait_pending_comm_ops waits for every scheduled item (lib.rs:321-337);
 //   * a monitor logs an op that runs longer than 300 s (lib.rs:255-265; the
 //     reference panics the process, here the failure is logged and kept).
+//   * cross-bucket pipelining (async mode, BAGUA_SCHED_LANES, default 2): bucket
+//     i of the registration order runs its ops on lane 1 + i % lanes of its
+//     communicator -- a view with its own streams (comm_internal.hpp) -- so the
+//     next bucket's compress prefix and enqueue overlap this bucket's exchange and
+//     tail instead of queueing behind them on one stream.  A bucket always uses
+//     the same lane (its executions stay in stream order), the worker issues every
+//     lane's ops in schedule order (the collective order every rank sees), and
+//     buckets with hierarchical ops or several communicators stay on lane 0.
 // No Python on this path: the worker never takes the GIL unless a bucket
 // carries a Python callback op (python_ffi_op.rs), which ctypes runs with it.
 #include <hip/hip_runtime.h>
@@ -52,6 +60,7 @@ struct BucketTensor {
 
 struct BaguaBucketC {
     std::string name;
+    int sched_index = 0;  // position in the scheduler's registration order (its lane)
     std::vector<BucketTensor> tensors;
     std::vector<bagua_bucket_op_t> ops;
     std::unordered_set<std::string> ready;  // tensor names marked ready (guarded by `mu`)
@@ -232,8 +241,27 @@ int execute_bucket(BaguaBucketC* b, const std::vector<BucketTensor>& tensors, co
     return rc != BAGUA_OK ? rc : (e == hipSuccess && e2 == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP);
 }
 
+// the bucket's ops moved onto lane `lane` of their communicator: every op on one
+// (non-hierarchical) communicator, else nothing changes (false)
+bool ops_on_lane(std::vector<bagua_bucket_op_t>* ops, int lane) {
+    BaguaSingleCommunicatorC* comm = nullptr;
+    for (const bagua_bucket_op_t& op : *ops) {
+        if (op.intranode) return false;
+        if (!op.comm) continue;
+        if (comm && op.comm != comm) return false;
+        comm = op.comm;
+    }
+    if (!comm || comm->parent) return false;
+    BaguaSingleCommunicatorC* view = comm->lane(lane);
+    if (!view) return false;
+    for (bagua_bucket_op_t& op : *ops)
+        if (op.comm) op.comm = view;
+    return true;
+}
+
 struct Scheduled {
     BaguaBucketC* bucket = nullptr;
+    int lane_hint = 0;                     // the bucket's registration index
     std::vector<BucketTensor> tensors;     // tensor descriptors at scheduling time
     std::vector<uint64_t> events;          // ready events at scheduling time
     std::vector<bagua_bucket_op_t> ops;    // the bucket's ops at scheduling time
@@ -258,6 +286,7 @@ struct BaguaCommBackendC {
     std::vector<std::string> failures;
     bool stop = false;
     bool async = true;                  // BAGUA_BACKEND_SYNC=1: every op waits for its stream
+    int lanes = 2;                      // BAGUA_SCHED_LANES (async only; 1 = every bucket on the comm's stream)
     std::vector<hipEvent_t> spare;      // completion events for reuse
     std::thread worker, monitor;
 
@@ -310,8 +339,15 @@ struct BaguaCommBackendC {
                 current_start = std::chrono::steady_clock::now();
             }
             const clk::time_point t_exec = clk::now();
-            hipStream_t s = ops_stream(item->ops);
-            const int rc = execute_bucket(item->bucket, item->tensors, item->events, item->ops, s);
+            int nl;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                nl = lanes;
+            }
+            std::vector<bagua_bucket_op_t> ops = item->ops;
+            if (async && nl > 1 && !ops_on_lane(&ops, 1 + item->lane_hint % nl)) ops = item->ops;
+            hipStream_t s = ops_stream(ops);
+            const int rc = execute_bucket(item->bucket, item->tensors, item->events, ops, s);
             const clk::time_point t_fin = clk::now();
             hipEvent_t fin = nullptr;
             if (async) {
@@ -467,6 +503,8 @@ BaguaCommBackendC* bagua_comm_backend_create(size_t schedule_channel_cap, int de
     const char* sync = std::getenv("BAGUA_BACKEND_SYNC");
     be->async = !(sync && *sync && std::atoi(sync) != 0);
     be->cap = schedule_channel_cap ? schedule_channel_cap : 1;
+    const char* ln = std::getenv("BAGUA_SCHED_LANES");
+    if (ln && *ln) be->lanes = std::max(1, std::min(8, std::atoi(ln)));
     const char* prof = std::getenv("BAGUA_SCHED_PROFILE");
     be->profile = prof && *prof && std::atoi(prof) != 0;
     be->worker = std::thread([be] { be->work(); });
@@ -550,6 +588,7 @@ int bagua_comm_backend_register_ordered_buckets(BaguaCommBackendC* be, BaguaBuck
     std::lock_guard<std::mutex> lk(be->mu);
     be->mapping.swap(mapping);
     be->ordered.assign(buckets, buckets + n);
+    for (int i = 0; i < n; ++i) buckets[i]->sched_index = i;
     return BAGUA_OK;
 }
 
@@ -577,6 +616,7 @@ int bagua_comm_backend_mark_communication_ready_desc(BaguaCommBackendC* be, cons
         if (be->stop) return BAGUA_ERR_INVALID_ARG;
         auto item = std::make_shared<Scheduled>();
         item->bucket = b;
+        item->lane_hint = b->sched_index;
         item->tensors = copy_tensors(b);
         item->events = take_events(b);
         item->ops = copy_ops(b);
@@ -585,6 +625,22 @@ int bagua_comm_backend_mark_communication_ready_desc(BaguaCommBackendC* be, cons
         be->cv_work.notify_all();
     }
     return BAGUA_OK;
+}
+
+int bagua_comm_backend_set_lanes(BaguaCommBackendC* be, int lanes) {
+    // waits for everything scheduled, so no bucket changes lane while in flight
+    if (!be || lanes < 1 || lanes > 8) return BAGUA_ERR_INVALID_ARG;
+    int done = 0;
+    const int rc = bagua_comm_backend_wait_pending_comm_ops(be, &done);
+    std::lock_guard<std::mutex> lk(be->mu);
+    be->lanes = lanes;
+    return rc;
+}
+
+int bagua_comm_backend_lanes(BaguaCommBackendC* be) {
+    if (!be) return -1;
+    std::lock_guard<std::mutex> lk(be->mu);
+    return be->async ? be->lanes : 1;
 }
 
 int bagua_comm_backend_failures(BaguaCommBackendC* be) {

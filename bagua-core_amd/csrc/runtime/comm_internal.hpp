@@ -15,6 +15,7 @@
 #include <atomic>
 #include <cstddef>
 #include <cstdlib>
+#include <mutex>
 #include <vector>
 
 namespace bagua {
@@ -61,6 +62,20 @@ struct BaguaSingleCommunicatorC {
     // async ops (bagua_comm_set_async, or the native scheduler's worker): an op returns
     // once its work is enqueued; buffers go back to the pool behind the stream
     bool async = false;
+    // Lane views (the scheduler's cross-bucket pipelining, backend.cpp): communicators
+    // that share this one's transport, rank and device but own their streams, side
+    // streams and events, so consecutive buckets' ops run on different streams and
+    // bucket b+1's codec prefix overlaps bucket b's exchange and tail.  RCCL runs the
+    // collectives of one communicator in issue order whatever the stream they are
+    // issued on, and the scheduler's one worker thread issues every lane's ops, so the
+    // collective order stays identical on every rank.  A view never owns the transport.
+    BaguaSingleCommunicatorC* parent = nullptr;
+    bool own_stream = false;
+    std::mutex lanes_mu;
+    std::vector<BaguaSingleCommunicatorC*> lanes;  // lanes[i] = view i + 1 (lane 0 is this one)
+
+    // lane `i` (0: this communicator itself); nullptr when its stream cannot be created
+    BaguaSingleCommunicatorC* lane(int i);
 
     int ensure_side(size_t n_events) {
         if (!side && hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) {
@@ -87,6 +102,7 @@ struct BaguaSingleCommunicatorC {
         return 0;
     }
     ~BaguaSingleCommunicatorC() {
+        for (BaguaSingleCommunicatorC* v : lanes) delete v;
         // per-stream workspaces and one-launch encode slots of the streams this
         // communicator ran ops on (the side stream is destroyed right after);
         // release waits for the streams, so an aborted communicator, whose
@@ -98,6 +114,7 @@ struct BaguaSingleCommunicatorC {
         for (hipEvent_t e : events) (void)hipEventDestroy(e);
         if (join) (void)hipEventDestroy(join);
         if (side) (void)hipStreamDestroy(side);
+        if (own_stream && stream && !aborted.load()) (void)hipStreamDestroy(stream);
     }
 };
 

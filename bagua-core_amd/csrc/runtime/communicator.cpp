@@ -128,6 +128,30 @@ Transport* make_rccl_transport(ncclComm_t comm) { return new RcclTransport(comm)
 
 using namespace bagua;
 
+BaguaSingleCommunicatorC* BaguaSingleCommunicatorC::lane(int i) {
+    if (i <= 0) return this;
+    std::lock_guard<std::mutex> g(lanes_mu);
+    while ((int)lanes.size() < i) {
+        DeviceGuard guard(device_id);
+        hipStream_t s = nullptr;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        auto* v = new BaguaSingleCommunicatorC();
+        v->t = t;
+        v->rank = rank;
+        v->nranks = nranks;
+        v->device_id = device_id;
+        v->stream = s;
+        v->own_stream = true;
+        v->parent = this;
+        v->async = async;
+        v->aborted.store(aborted.load());
+        // lanes run codec work beside each other: no one-launch encode (it needs every CU)
+        (void)bagua_minmax_u8_set_stream_resident(s, 0);
+        lanes.push_back(v);
+    }
+    return lanes[(size_t)i - 1];
+}
+
 #define COMM_CHECK(c)                                        \
     do {                                                     \
         if (!(c) || !(c)->t) return BAGUA_ERR_INVALID_ARG;   \
@@ -198,7 +222,12 @@ uint64_t bagua_single_communicator_c_stream(BaguaSingleCommunicatorC* c) {
 int bagua_comm_abort(BaguaSingleCommunicatorC* c) {
     // communicators/mod.rs:456-466
     if (!c) return BAGUA_ERR_INVALID_ARG;
+    if (c->parent) c = c->parent;  // a lane view aborts the communicator it shares
     c->aborted.store(true);
+    {
+        std::lock_guard<std::mutex> g(c->lanes_mu);
+        for (BaguaSingleCommunicatorC* v : c->lanes) v->aborted.store(true);
+    }
     return c->t ? c->t->abort() : BAGUA_OK;
 }
 

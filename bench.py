@@ -145,6 +145,8 @@ def parse():
     ap.add_argument("--workload", choices=["auto", "codec", "allreduce", "onebit", "host", "backend"], default="auto")
     ap.add_argument("--buckets", type=int, default=32, help="backend workload: gradient buckets per iteration")
     ap.add_argument("--bucket-mib", type=int, default=25, help="backend workload: MiB of fp32 gradient per bucket")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="backend workload: scheduler lanes (cross-bucket pipelining; 0 = the library default)")
     ap.add_argument("--elements", type=int, default=0, help="override bucket elements")
     ap.add_argument("--dtype", choices=["f32", "f16", "bf16"], default="f32",
                     help="codec workloads: gradient dtype (the headline is f32; bf16/f16 buckets keep 256 MiB)")
@@ -880,6 +882,25 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         comm.handle, ctypes.byref(small), 1, N.COMPRESSION_MINMAX_UINT8, user_pieces), "25 MiB op"))
     t_sf = side("bucket_25mib_fp32", lambda: N.check(N.C.bagua_centralized_full_precision_synchronous(
         comm.handle, ctypes.byref(small), 1), "25 MiB fp32 allreduce"))
+    # the scheduler workload (32 x 25 MiB buckets, Bagua's default bucket size) through the native
+    # scheduler on this communicator: cross-bucket lanes (the default) and one lane, so the node's
+    # run shows how much of each bucket's codec prefix the next bucket's exchange hides
+    sched = {}
+    nbk, mib = (32, 25) if not args.elements else (8, max(1, (4 * n >> 20) // 8))  # --elements: a rehearsal
+    if world > 1:
+        try:
+            wl = SchedulerWorkload(comm, world, rank, local_rank, nbk, mib)
+            sched["buckets"], sched["bucket_mib"] = nbk, mib
+            for ln in (wl.backend.lanes(), 1):
+                wl.backend.set_lanes(ln)
+                t_sc = side(f"scheduler_lanes{ln}", wl.iteration)
+                sched[f"lanes_{ln}"] = {"ms_per_step": round(t_sc * 1e3, 4),
+                                        "per_bucket_us": round(t_sc * 1e6 / nbk, 2),
+                                        "gib_s_total": round(world * 4.0 * wl.per * nbk / t_sc / GiB, 2)}
+            wl.close()
+            del wl
+        except Exception as e:  # noqa: BLE001 - a failed side measurement must not lose the headline line
+            side_errors.setdefault("scheduler", str(e)[:200])
     t_o = side("onebit", onebit_step)
     t_ou = side("onebit_unpieced", lambda: onebit_step(1))
     decentralized = None
@@ -970,6 +991,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
                               "gib_s_total": round(world * 4.0 * m / t_s / GiB, 2),
                               "ratio_vs_fp32": round(t_sf / t_s, 3)},
              "decentralized_bf16": decentralized,
+             "scheduler_buckets": sched or None,
              "onebit_allreduce": {"ms_per_step": round(t_o * 1e3, 3), "unpieced_ms_per_step": round(t_ou * 1e3, 3),
                                   "per_rank_gib_s": round(4.0 * n / t_o / GiB, 2),
                                   "ratio_vs_fp32": round((4.0 * n / t_o) / (4.0 * n / t_f), 3)},
@@ -982,13 +1004,82 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     return value, t_c * 1e3, roof, cfg, extra
 
 
+class SchedulerWorkload:
+    """The scheduler (BaguaCommBackendPy, bagua-core-internal/src/lib.rs:176-338) driving a
+    model-sized gradient: `buckets` buckets of `bucket_mib` MiB fp32 (4 tensors each,
+    contiguous), each with the compressed centralized op on `comm`.  One iteration =
+    every tensor marked ready in reverse bucket order (as backward produces them, each
+    bucket with a ready event) + wait_pending_comm_ops."""
+
+    def __init__(self, comm, world: int, rank: int, local_rank: int, buckets: int, bucket_mib: int):
+        import bagua_core
+        dev = torch.device("cuda", local_rank)
+        self.world, self.nb = world, buckets
+        per = (bucket_mib << 20) // 4
+        per -= per % (4 * 32 * world)
+        self.per = per
+        g = torch.Generator(device=dev).manual_seed(0x5EED + rank)
+        self.flats = [torch.randn(per, device=dev, generator=g) * 1e-3 for _ in range(buckets)]
+        self.buckets, self.tensors = [], []
+        for b, flat in enumerate(self.flats):
+            ts = [bagua_core.BaguaTensorPy(v, f"b{b}.t{i}") for i, v in enumerate(flat.view(4, -1).unbind(0))]
+            bk = bagua_core.BaguaBucketPy(f"bucket{b}", ts)
+            bk.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+            self.buckets.append(bk)
+            self.tensors.append(ts)
+        self.backend = bagua_core.BaguaCommBackendPy(buckets, local_rank)
+        # backward produces the last layers' gradients first: the registration order is the
+        # order buckets become ready
+        self.backend.register_ordered_buckets(list(reversed(self.buckets)))
+        self.events = [torch.cuda.Event() for _ in range(buckets)]
+        # where backward's ready events are recorded: the current (default) stream, as a
+        # training loop does, or a stream of their own (BAGUA_BENCH_READY_STREAM=own, A/B)
+        self.ready_mode = os.environ.get("BAGUA_BENCH_READY_STREAM", "default")  # default / own / none
+        self.ready_stream = torch.cuda.Stream(device=dev) if self.ready_mode == "own" else None
+        self.mark_s = []
+        torch.cuda.synchronize()
+
+    def iteration(self):
+        t0 = time.perf_counter()
+        for b in reversed(range(self.nb)):
+            if self.ready_mode != "none":
+                self.events[b].record(self.ready_stream)
+            ev = self.events[b].cuda_event if self.ready_mode != "none" else 0
+            for t in self.tensors[b]:
+                self.backend.mark_communication_ready(t, ev)
+        self.mark_s.append(time.perf_counter() - t0)
+        done = self.backend.wait_pending_comm_ops()
+        assert done == self.nb, done
+
+    def time(self, steps: int, warmup: int, lanes: int, barrier=None) -> float:
+        """ms per iteration (max over ranks when `barrier` reduces)"""
+        self.backend.set_lanes(lanes)
+        for _ in range(max(1, warmup)):
+            self.iteration()
+        torch.cuda.synchronize()
+        if barrier:
+            barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.iteration()
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        if self.world > 1:
+            import torch.distributed as dist
+            tt = torch.tensor([t], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t = float(tt.item())
+        return t / steps * 1e3
+
+    def close(self):
+        del self.backend, self.buckets
+
+
 def bench_backend(args, world: int, rank: int, local_rank: int):
-    """The scheduler (BaguaCommBackendPy, bagua-core-internal/src/lib.rs:176-338)
-    driving a model-sized gradient: `--buckets` buckets of `--bucket-mib` MiB fp32
-    (4 tensors each, contiguous), each with the compressed centralized op.  One
-    iteration = every tensor marked ready in reverse bucket order (as backward
-    produces them, each with a ready event) + wait_pending_comm_ops.  value = GiB of
-    gradient per second (all ranks)."""
+    """The scheduler workload (SchedulerWorkload): `--buckets` x `--bucket-mib` MiB fp32
+    buckets through the native scheduler, with cross-bucket lanes (backend.cpp; the
+    default 2) and, beside it, one lane (every bucket on the communicator's stream).
+    value = GiB of gradient per second (all ranks)."""
     import torch.distributed as dist
     import bagua_core
     dev = torch.device("cuda", local_rank)
@@ -1000,64 +1091,25 @@ def bench_backend(args, world: int, rank: int, local_rank: int):
         dist.broadcast_object_list(uid, src=0)
     comm_stream = torch.cuda.Stream(device=dev)
     comm = bagua_core.BaguaSingleCommunicatorPy(rank, world, local_rank, comm_stream.cuda_stream, uid[0])
-    per = (args.bucket_mib << 20) // 4
-    per -= per % (4 * 32 * world)
-    g = torch.Generator(device=dev).manual_seed(0x5EED + rank)
-    flats = [torch.randn(per, device=dev, generator=g) * 1e-3 for _ in range(args.buckets)]
-    buckets, tensors = [], []
-    for b, flat in enumerate(flats):
-        ts = [bagua_core.BaguaTensorPy(v, f"b{b}.t{i}") for i, v in enumerate(flat.view(4, -1).unbind(0))]
-        bk = bagua_core.BaguaBucketPy(f"bucket{b}", ts)
-        bk.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
-        buckets.append(bk)
-        tensors.append(ts)
-    backend = bagua_core.BaguaCommBackendPy(args.buckets, local_rank)
-    # backward produces the last layers' gradients first: the registration order is the
-    # order buckets become ready
-    backend.register_ordered_buckets(list(reversed(buckets)))
-    events = [torch.cuda.Event() for _ in range(args.buckets)]
-    # where backward's ready events are recorded: the current (default) stream, as a
-    # training loop does, or a stream of their own (BAGUA_BENCH_READY_STREAM=own, A/B)
-    ready_mode = os.environ.get("BAGUA_BENCH_READY_STREAM", "default")  # default / own / none (no ready events)
-    ready_stream = torch.cuda.Stream(device=dev) if ready_mode == "own" else None
-
-    mark_s = []
-
-    def iteration():
-        t0 = time.perf_counter()
-        for b in reversed(range(args.buckets)):
-            if ready_mode != "none":
-                events[b].record(ready_stream)
-            for t in tensors[b]:
-                backend.mark_communication_ready(t, events[b].cuda_event if ready_mode != "none" else 0)
-        mark_s.append(time.perf_counter() - t0)
-        done = backend.wait_pending_comm_ops()
-        assert done == args.buckets, done
-
-    for _ in range(max(1, args.warmup)):
-        iteration()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        iteration()
-    torch.cuda.synchronize()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    if world > 1:
-        dist.barrier()
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    ms = float(t.item()) / args.steps * 1e3
-    grad_bytes = 4.0 * per * args.buckets
+    wl = SchedulerWorkload(comm, world, rank, local_rank, args.buckets, args.bucket_mib)
+    barrier = (lambda: dist.barrier()) if world > 1 else None
+    lanes = args.lanes or wl.backend.lanes()
+    ms = wl.time(args.steps, args.warmup, lanes, barrier)
+    mark = sorted(wl.mark_s)[len(wl.mark_s) // 2]
+    ms1 = wl.time(args.steps, args.warmup, 1, barrier) if lanes != 1 else ms
+    grad_bytes = 4.0 * wl.per * args.buckets
     value = world * grad_bytes / (ms * 1e-3) / GiB
     cfg = {"workload": f"comm_backend_{args.buckets}x{args.bucket_mib}MiB_fp32_buckets_minmax_uint8",
-           "bucket_elements": per, "buckets": args.buckets, "tensors_per_bucket": 4,
-           "parallelism": f"dp{world}", "scheduler": type(backend).__module__ + "." + type(backend).__name__}
+           "bucket_elements": wl.per, "buckets": args.buckets, "tensors_per_bucket": 4,
+           "parallelism": f"dp{world}", "scheduler": "bagua_core.backend.BaguaCommBackendPy", "lanes": lanes}
     extra = {"per_bucket_us": round(ms * 1e3 / args.buckets, 2), "per_rank_gib_s": round(value / world, 2),
              # host time of the Python side per bucket (a ready event + one mark per tensor): the
              # scheduler cannot run a bucket before its last tensor is marked
-             "mark_us_per_bucket": round(sorted(mark_s)[len(mark_s) // 2] * 1e6 / args.buckets, 2)}
-    del backend, buckets, comm
+             "mark_us_per_bucket": round(mark * 1e6 / args.buckets, 2),
+             "one_lane": {"ms_per_step": round(ms1, 4), "per_bucket_us": round(ms1 * 1e3 / args.buckets, 2),
+                          "gib_s_total": round(world * grad_bytes / (ms1 * 1e-3) / GiB, 2)}}
+    wl.close()
+    del comm
     return value, ms, None, cfg, extra
 
 

@@ -305,6 +305,14 @@ int bagua_comm_backend_mark_communication_ready_desc(BaguaCommBackendC* backend,
 int bagua_comm_backend_wait_pending_comm_ops(BaguaCommBackendC* backend, int* completed);
 /* ops the monitor saw running longer than 300 s (lib.rs:255-265) */
 int bagua_comm_backend_failures(BaguaCommBackendC* backend);
+/* Cross-bucket pipelining (no reference counterpart): bucket i of the registration
+ * order runs on lane 1 + i % lanes of its communicator -- a view with its own
+ * streams -- so consecutive buckets overlap on the GPU; 1 = every bucket on the
+ * communicator's stream (the reference's one stream).  Default 2 (BAGUA_SCHED_LANES),
+ * async schedulers only.  set_lanes first waits for everything scheduled;
+ * bagua_comm_backend_lanes returns the lanes in effect. */
+int bagua_comm_backend_set_lanes(BaguaCommBackendC* backend, int lanes);
+int bagua_comm_backend_lanes(BaguaCommBackendC* backend);
 
 #ifdef __cplusplus
 }

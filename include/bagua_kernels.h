@@ -104,6 +104,10 @@ int bagua_minmax_u8_resident_trace(void* device_buffer);
  * counter read on a private stream: no other stream is synchronised); when all
  * slots are owned, the least recently used one is reclaimed the same way. */
 int bagua_minmax_u8_release_stream(bagua_stream_t stream);
+/* allowed = 0: compress calls on `stream` always take the two-pass encode (a stream
+ * that runs codec work beside another codec stream, e.g. the scheduler's lanes);
+ * 1 (the default) restores the one-launch encode.  Releasing the stream resets it. */
+int bagua_minmax_u8_set_stream_resident(bagua_stream_t stream, int allowed);
 /* Streams currently holding a slot on `device_id` (tests and diagnostics). */
 int bagua_minmax_u8_resident_slots_in_use(int device_id);
 /* measurement: how many workgroups of `stream`'s one-launch encodes timed out waiting

@@ -56,8 +56,9 @@ def _grads(n_buckets, per, seed, scattered=False):
     return host, [list(f.view(3, -1).unbind(0)) if per % 3 == 0 else [f] for f in flats], flats
 
 
+@pytest.mark.parametrize("lanes", [1, 2, 3])
 @pytest.mark.parametrize("scattered", [False, True])
-def test_scheduler_runs_buckets_in_order_and_matches_oracle(bc, comm, oracle_c, scattered):
+def test_scheduler_runs_buckets_in_order_and_matches_oracle(bc, comm, oracle_c, scattered, lanes):
     n_buckets, per = 6, 3 * 40000
     host, parts, _keep = _grads(n_buckets, per, 7 + scattered, scattered)
     log = []
@@ -70,6 +71,8 @@ def test_scheduler_runs_buckets_in_order_and_matches_oracle(bc, comm, oracle_c, 
         buckets.append(bk)
         tensors.append(ts)
     backend = bc.BaguaCommBackendPy(2, 0)
+    backend.set_lanes(lanes)  # cross-bucket pipelining: bucket i on lane 1 + i % lanes
+    assert backend.lanes() == lanes
     backend.register_ordered_buckets(buckets)
     ev = torch.cuda.Event()
     # mark the LAST bucket first: nothing may run until bucket 0 is ready
@@ -226,10 +229,11 @@ def test_backend_sync_mode_env(bc, comm, oracle_c, monkeypatch):
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
-@pytest.mark.parametrize("p", [2, 4])
-def test_scheduler_multirank_loopback(bc, oracle_c, p):
+@pytest.mark.parametrize("p,lanes", [(2, 1), (2, 2), (4, 2), (4, 3)])
+def test_scheduler_multirank_loopback(bc, oracle_c, p, lanes):
     """p virtual ranks on the loopback transport, each with its own scheduler (worker
-    thread, async ops) and the same ordered buckets: every rank's workers meet in the
+    thread, async ops, `lanes` streams per communicator for consecutive buckets) and the
+    same ordered buckets: every rank's workers meet in the
     collectives, and every bucket on every rank equals the oracle's simulation of the
     reference op across the ranks (bit-for-bit).  Buckets are marked ready in reverse
     order, as backward produces them; the scheduler runs them in registration order."""
@@ -251,6 +255,7 @@ def test_scheduler_multirank_loopback(bc, oracle_c, p):
             buckets.append(bk)
             ts_r.append(ts)
         be = bc.BaguaCommBackendPy(2, 0)
+        be.set_lanes(lanes)
         be.register_ordered_buckets(buckets)
         backends.append((be, buckets))
         tensors.append(ts_r)
@@ -358,3 +363,50 @@ def test_execute_on_a_foreign_stream_orders_the_pack(bc, comm, oracle_c):
     want = simulate.centralized_low_precision(oracle_c, [h], F32, True)[0]
     got = torch.cat(parts).cpu().numpy()
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_lanes_pipelined_op_buckets(bc, oracle_c, lanes):
+    """Cross-bucket lanes with the pipelined op at p = 2 (side stream per lane, pieces
+    exchanged on the loopback transport) over buckets large enough to be pieced, two
+    iterations without re-registration: every bucket equals the oracle simulation."""
+    from bagua_core.communicator import loopback_communicators
+    p, n_buckets, per = 2, 4, 2 * (1 << 21)
+    comms = loopback_communicators(p, 0)
+    rng = np.random.default_rng(300 + lanes)
+    host = [[(rng.standard_normal(per) * 1e-3).astype(np.float32) for _ in range(n_buckets)] for _ in range(p)]
+    flats = [[torch.from_numpy(h.copy()).cuda() for h in host[r]] for r in range(p)]
+    backends, tensors = [], []
+    for r in range(p):
+        buckets, ts_r = [], []
+        for b in range(n_buckets):
+            t = bc.BaguaTensorPy(flats[r][b], f"g{b}")
+            bk = bc.BaguaBucketPy(f"bucket{b}", [t])
+            bk.append_centralized_synchronous_op(comms[r], None, False, True, False, "MinMaxUInt8")
+            buckets.append(bk)
+            ts_r.append(t)
+        be = bc.BaguaCommBackendPy(4, 0)
+        be.set_lanes(lanes)
+        be.register_ordered_buckets(buckets)
+        backends.append((be, buckets))
+        tensors.append(ts_r)
+    torch.cuda.synchronize()
+    for it in range(2):
+        done = [None] * p
+
+        def rank(r):
+            for b in reversed(range(n_buckets)):
+                backends[r][0].mark_communication_ready(tensors[r][b], 0)
+            done[r] = backends[r][0].wait_pending_comm_ops()
+        ths = [threading.Thread(target=rank, args=(r,)) for r in range(p)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join(timeout=120)
+        assert done == [n_buckets] * p, done
+        for b in range(n_buckets):
+            want = simulate.centralized_low_precision(oracle_c, [host[r][b] for r in range(p)], F32, True)
+            for r in range(p):
+                host[r][b] = want[r]
+                assert np.array_equal(flats[r][b].cpu().numpy().view(np.uint32), want[r].view(np.uint32)), (it, b, r)
+    del backends

@@ -205,6 +205,8 @@ def test_bench_line_multirank(tmp_path, world, fail_headline, launcher):
         assert d["pieces"] == int(best.split("_")[0]) and d["pieces_tapered"] == best.endswith("_tapered"), d
         assert all(v > 0 for v in d["pieces_sweep_ms_per_step"].values()), d["pieces_sweep_ms_per_step"]
     assert d["roofline"]["frac"] > 0
+    sc = d["scheduler_buckets"]  # the native scheduler over this RCCL communicator, lanes and one lane
+    assert sc and sc["lanes_1"]["ms_per_step"] > 0 and len([k for k in sc if k.startswith("lanes_")]) == 2, sc
     # the CPU path beside every N: rank 0 runs the op sequence for all ranks on the host cores
     c = d["cpu_baseline"]
     assert c and c["value"] > 0 and c["cores"] >= 1 and c["host"]["os_cpu_count"] >= 1 and str(world) in c["sample"]
