@@ -84,6 +84,7 @@ KERNEL_SIGNATURES = {
     "bagua_minmax_u8_resident_trace": (_i32, [_vp]),
     "bagua_minmax_u8_release_stream": (_i32, [_vp]),
     "bagua_minmax_u8_set_stream_resident": (_i32, [_vp, _i32]),
+    "bagua_minmax_u8_centralized_one_rank": (_i32, [_i32, _vp, _i32, _i32, _vp, _sz, _vp]),
     "bagua_minmax_u8_resident_slots_in_use": (_i32, [_i32]),
     "bagua_minmax_u8_resident_give_ups": (_i32, [_vp, ctypes.POINTER(_u64)]),
     "bagua_minmax_u8_decompress_reduce": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _vp]),

@@ -294,6 +294,128 @@ __global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
 }
 
 // ------------------------------------------------------------------------
+// the centralized op at ONE rank, after the min/max pass (p = 1)
+// ------------------------------------------------------------------------
+// centralized_low_precision_synchronous.rs:30-71 with one rank is, per element,
+//   b1 = Q1(x)                 compress, header1 = min/max of x
+//   y  = T(T(dq1(b1)) + 0 + 0) decompress, then reduce over one chunk (K:373-400:
+//                              s = 0.0f + c0, the BY = 2 tree adds 0.0f; mean: x 1)
+//   b2 = Q2(y)                 compress, header2 = min/max of y (as stored in T)
+//   out = T(dq2(b2))           decompress
+// so `out` is a function of b1 alone: a 256-entry table per launch.  header2
+// needs no pass over y:
+//  * header1 finite and scale1 finite > 0: Q1 (x*scale, rint, fminf(ub), - lb,
+//    saturate) and dq1 ((b + lb) / scale, then T rounding, + 0.0f) are monotone
+//    non-decreasing, and Q1(NaN) = Q1(max) (fminf(NaN, ub) = ub), so
+//    min y = y(Q1(min x)) and max y = y(Q1(max x)), both finite or +-inf, never
+//    NaN (dq1 of a finite lb over a positive scale);
+//  * every element NaN (header = the init values, min > max): every b1 is Q1(NaN),
+//    so y takes one value, header2 = (y, y) -- or the init values if y is NaN;
+//  * otherwise (a +-inf in the header, or max - min overflowing: scale1 is +0 or
+//    NaN) every b1 decodes to NaN -- scale1 = +0 comes with every byte 255 (mx
+//    finite: (255 + lb)/0 = 0/0) or every byte 0 with lb NaN -- so header2 is the
+//    min/max over no value: the init values (T::init_max, -T::init_max).
+// Bit-identical to the four-kernel sequence (tests/test_gpu_codec.py
+// test_one_rank_op_matches_sequence, incl. NaN, +-inf and all-NaN buckets); reads
+// 4N and writes 4N bytes after the 4N of the min/max pass (12N) instead of 18N.
+template <typename T, int AV>
+__device__ __forceinline__ float one_rank_reduce(float c0) {
+    float s = 0.0f + c0;  // s[0] of the BY = 2 tree
+    s = s + 0.0f;         // + s[1] (no second chunk)
+    if constexpr (AV == 0) return s;
+    else return s * 1.0f;  // mean over p = 1: the exact reciprocal (reduce.hip avg_finish)
+}
+
+template <typename T, int AV>
+__global__ __launch_bounds__(kBlock) void minmax_one_rank_kernel(typename T::storage* __restrict__ x, int64_t n,
+                                                                 const uint2* __restrict__ partials, int npartials) {
+    using S = typename T::storage;
+    constexpr int N = Vec<T>::N;
+    uint32_t lo = 0xffffffffu, hi = 0xffffffffu;
+    for (int i = threadIdx.x; i < npartials; i += kBlock) {
+        const uint2 p = partials[i];
+        lo = min(lo, p.x);
+        hi = min(hi, p.y);
+    }
+    lo = wave_umin(lo);
+    hi = wave_umin(hi);
+    __shared__ uint32_t red[2][kWavesPerBlock];
+    __shared__ uint32_t lut[256];  // b1 -> the T bits of the op's final value
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 0) { red[0][w] = lo; red[1][w] = hi; }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
+    const float mn1 = from_min_space(lo), mx1 = from_max_space(hi);
+    const QParams q1 = make_qparams(mn1, mx1);
+    const bool regular = __builtin_isfinite(mn1) && __builtin_isfinite(mx1) && __builtin_isfinite(q1.scale) &&
+                         q1.scale > 0.0f;
+    auto y_of = [&](uint32_t b) { return as_stored<T>(one_rank_reduce<T, AV>(as_stored<T>(dequant(b, q1)))); };
+    float mn2 = T::init_max(), mx2 = -T::init_max();
+    if (regular) {
+        mn2 = y_of(quant(mn1, q1));
+        mx2 = y_of(quant(mx1, q1));
+    } else if (!(mn1 <= mx1)) {
+        // every element NaN (the header holds the init values): one byte value for all of
+        // them, so one y value -- the min and max of y unless it is NaN itself (the f16
+        // init header has a finite, negative scale: y = -inf there)
+        const float ys = y_of(quant(__int_as_float(0x7fc00000), q1));
+        if (!__builtin_isnan(ys)) mn2 = mx2 = ys;
+    }
+    const QParams q2 = make_qparams(mn2, mx2);
+    static_assert(kBlock == 256, "one table entry per thread");
+    lut[threadIdx.x] = stored_bits<T>(dequant(quant(y_of(threadIdx.x), q2), q2));
+    __syncthreads();
+
+    // the body on 16-B vectors (head elements before the first aligned one go scalar)
+    int64_t j0 = (int64_t)(((16u - ((uintptr_t)x & 15u)) & 15u) / sizeof(S));
+    if (((uintptr_t)x % sizeof(S)) != 0) j0 = n;
+    if (j0 > n) j0 = n;
+    const int64_t nvec = (n - j0) / N;
+    uint4* __restrict__ v = reinterpret_cast<uint4*>(x + j0);
+    const int64_t ntiles = (nvec + kVecPerBlockTile - 1) / kVecPerBlockTile;
+    // reverse sweep: the min/max pass read the tail last, so it is re-read from the
+    // Infinity Cache first
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int64_t base = (ntiles - 1 - t) * kVecPerBlockTile;
+        if (base + kVecPerBlockTile <= nvec) {
+            uint4 r[kSubtiles];
+#pragma unroll
+            for (int k = 0; k < kSubtiles; ++k) r[k] = nt_load16(&v[base + k * kBlock + threadIdx.x]);
+#pragma unroll
+            for (int k = 0; k < kSubtiles; ++k) {
+                float f[N];
+                unpack16<T>(r[k], f);
+                uint32_t b[N];
+#pragma unroll
+                for (int i = 0; i < N; i += 4) {
+                    const uint32_t q = quant_pack4(f[i], f[i + 1], f[i + 2], f[i + 3], q1);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) b[i + e] = lut[(q >> (8 * e)) & 0xff];
+                }
+                nt_store16(pack_stored<T>(b), &v[base + k * kBlock + threadIdx.x]);
+            }
+            continue;
+        }
+        for (int k = 0; k < kSubtiles; ++k) {
+            const int64_t vi = base + k * kBlock + threadIdx.x;
+            if (vi >= nvec) continue;
+            float f[N];
+            unpack16<T>(nt_load16(&v[vi]), f);
+            uint32_t b[N];
+#pragma unroll
+            for (int i = 0; i < N; ++i) b[i] = lut[quant(f[i], q1)];
+            nt_store16(pack_stored<T>(b), &v[vi]);
+        }
+    }
+    if (blockIdx.x == 0) {
+        for (int64_t j = threadIdx.x; j < j0; j += kBlock) x[j] = storage_from_bits<T>(lut[quant(T::to_f(x[j]), q1)]);
+        for (int64_t j = j0 + nvec * N + threadIdx.x; j < n; j += kBlock)
+            x[j] = storage_from_bits<T>(lut[quant(T::to_f(x[j]), q1)]);
+    }
+}
+
+// ------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------
 // workgroups per chunk: one per tile of (kBlock * sub) vectors, capped so the
@@ -510,6 +632,26 @@ static int requantize_pieces_impl(const void* tensor, int cs, int p, uint8_t* ou
 }
 
 template <typename T>
+static int one_rank_impl(void* tensor, int num_elem, int average, void* ws, size_t ws_bytes, hipStream_t s) {
+    using S = typename T::storage;
+    if (!tensor || num_elem < 0) return BAGUA_ERR_INVALID_ARG;
+    const int nblk = ws ? minmax_partials_blocks(num_elem, Vec<T>::N, 1, ws_bytes) : 0;
+    if (nblk < 1) return BAGUA_ERR_WORKSPACE;
+    uint2* partials = static_cast<uint2*>(ws);
+    launch(minmax_partials_kernel<T>, dim3(nblk, 1), dim3(kBlock), 0, s, static_cast<const S*>(tensor),
+           (int64_t)num_elem, (int64_t)num_elem, -1, partials);
+    const dim3 grid(blocks_for(num_elem, Vec<T>::N, 1, kSubtiles, tune_int("BAGUA_TUNE_QUANT_BLOCKS", kQuantBlocks)),
+                    1);
+    if (average)
+        launch(minmax_one_rank_kernel<T, 1>, grid, dim3(kBlock), 0, s, static_cast<S*>(tensor), (int64_t)num_elem,
+               static_cast<const uint2*>(partials), nblk);
+    else
+        launch(minmax_one_rank_kernel<T, 0>, grid, dim3(kBlock), 0, s, static_cast<S*>(tensor), (int64_t)num_elem,
+               static_cast<const uint2*>(partials), nblk);
+    return check_launch();
+}
+
+template <typename T>
 static int decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, hipStream_t s,
                            int e0 = 0, int e1 = -1) {
     using S = typename T::storage;
@@ -627,6 +769,17 @@ int bagua_minmax_u8_reduce_requantize_final(int dtype, const uint8_t* input, siz
         case BAGUA_DTYPE_BF16:
             return reduce_requantize_impl<BF16>(input, input_bytes, chunk_size, num_chunks, nullptr, average, output,
                                                 output_bytes, target_chunk, workspace, workspace_bytes, s, tensor);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+int bagua_minmax_u8_centralized_one_rank(int dtype, void* tensor, int num_elem, int average, void* workspace,
+                                         size_t workspace_bytes, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32: return one_rank_impl<F32>(tensor, num_elem, average, workspace, workspace_bytes, s);
+        case BAGUA_DTYPE_F16: return one_rank_impl<F16>(tensor, num_elem, average, workspace, workspace_bytes, s);
+        case BAGUA_DTYPE_BF16: return one_rank_impl<BF16>(tensor, num_elem, average, workspace, workspace_bytes, s);
     }
     return BAGUA_ERR_UNSUPPORTED;
 }

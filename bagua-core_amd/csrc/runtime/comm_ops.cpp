@@ -168,6 +168,20 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
     if (rc) return rc;
     DeviceGuard guard(c->device_id);
     const uint64_t s = (uint64_t)(uintptr_t)c->stream;
+    if (k.p == 1 && fused && method == BAGUA_COMPRESSION_MINMAX_UINT8 && t->num_elem == t->num_elem_allocated &&
+        k.cs <= 0x7fffffffULL && env_int("BAGUA_ONE_RANK_FUSED", 1) != 0) {
+        // one rank: the whole sequence as the min/max pass + one table-driven pass over the
+        // tensor (bagua_minmax_u8_centralized_one_rank: the second header follows from the
+        // first), no compressed buffer at all; BAGUA_ONE_RANK_FUSED=0: the steps below (A/B)
+        const size_t ws_bytes = bagua_minmax_u8_workspace_bytes((int)k.cs, 1);
+        uint64_t ws = 0;
+        if ((rc = stream_workspace(c->device_id, s, ws_bytes, &ws)) != BAGUA_OK) return finish(c, rc);
+        ph[0] = tm.lap();
+        rc = bagua_minmax_u8_centralized_one_rank(t->dtype, (void*)(uintptr_t)t->ptr, (int)k.cs, average,
+                                                  (void*)(uintptr_t)ws, ws_bytes, (void*)(uintptr_t)s);
+        ph[2] = tm.lap();
+        return finish(c, rc);
+    }
     // 2. (below) alltoall: slot j of recv <- rank j's segment `rank`.  One rank receives
     // its own bytes: the MinMax steps below read them from `send` itself (their reads and
     // the requantise's writes are separate kernels in stream order; no recv buffer), the

@@ -201,6 +201,15 @@ int bagua_minmax_u8_reduce_requantize_final(int dtype, const uint8_t* input, siz
                                             size_t output_bytes, int target_chunk, void* workspace,
                                             size_t workspace_bytes, bagua_stream_t stream);
 
+/* The whole compressed centralized op at ONE rank
+ * (centralized_low_precision_synchronous.rs:30-71 with num_chunks = 1), in place:
+ * tensor <- decompress(compress(reduce(decompress(compress(tensor))))), two kernels
+ * (the min/max pass, then one pass whose output is a 256-entry table of the first
+ * quantised byte; the second header follows from the first).
+ * Bit-identical to the op's sequence; every element valid (num_elem elements). */
+int bagua_minmax_u8_centralized_one_rank(int dtype, void* tensor, int num_elem, int average, void* workspace,
+                                         size_t workspace_bytes, bagua_stream_t stream);
+
 /* Pipelined all-reduce building blocks (no reference counterpart: the same
  * kernels restricted to part of every chunk, so communication of one piece
  * overlaps the codec work of the next).  A chunk splits into `pieces` element

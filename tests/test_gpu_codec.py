@@ -514,3 +514,43 @@ def test_time_next_kernel_records_one_launch(bc):
                                              ctypes.c_void_p(st.cuda_stream)), "quantise")
     torch.cuda.synchronize()
     assert a.elapsed_time(b) == t1
+
+
+@pytest.mark.parametrize("dtype", [F32, F16, BF16])
+@pytest.mark.parametrize("case", ["normal", "offset", "nan_mixed", "pos_inf", "both_inf", "all_nan", "constant",
+                                  "huge_range", "tiny"])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_one_rank_op_matches_sequence(bc, oracle_c, dtype, case, offset):
+    """bagua_minmax_u8_centralized_one_rank (min/max pass + one table-driven pass) ==
+    the reference op sequence at p = 1 (centralized_low_precision_synchronous.rs:30-71:
+    compress, decompress, reduce, compress, decompress), regular and degenerate regimes,
+    aligned and misaligned tensors, mean and sum."""
+    from oracle import oracle_np as NP
+    from oracle import simulate
+    K = bc._native.K
+    rng = np.random.default_rng(len(case) * 7 + dtype + offset)
+    n = 5 if case == "tiny" else (1 << 20) + 37
+    big = {F32: 3e38, F16: 6e4, BF16: 3e38}[dtype]
+    v = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+    if case == "offset":
+        v += 7.5
+    elif case == "nan_mixed":
+        v[::7] = np.nan
+    elif case == "pos_inf":
+        v[5] = np.inf
+    elif case == "both_inf":
+        v[3], v[4] = np.inf, -np.inf
+    elif case == "all_nan":
+        v[:] = np.nan
+    elif case == "constant":
+        v[:] = 0.25
+    elif case == "huge_range":
+        v[0], v[1] = big, -big
+    x = NP.from_f32(v, dtype)
+    wsb = K.bagua_minmax_u8_workspace_bytes(n, 1)
+    ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+    for average in (1, 0):
+        want = simulate.centralized_low_precision(oracle_c, [x.copy()], dtype, bool(average))[0]
+        xt = to_dev(x, dtype, offset)
+        assert K.bagua_minmax_u8_centralized_one_rank(dtype, xt.data_ptr(), n, average, ws.data_ptr(), wsb, None) == 0
+        assert_float_bits_equal(to_host(xt, dtype), want, dtype, f"one rank {case} average={average}")

@@ -58,6 +58,7 @@ def test_centralized_op_fixtures(bc, goldens, variant):
     from bagua_core.communicator import loopback_communicators
     for i in _cases(goldens, "cen", 3):
         dtype, p, cs = (int(v) for v in goldens[f"cen_meta_{i}"])
+        print(f"cen case {i}: dtype {dtype} p {p} cs {cs} {variant}", flush=True)
         xs = [_arr(r, dtype) for r in goldens[f"cen_in_{i}"]]
         want = goldens[f"cen_out_{i}"]
         comms = loopback_communicators(p, 0)
