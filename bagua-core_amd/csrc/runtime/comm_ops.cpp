@@ -307,11 +307,56 @@ bool valid_schedule(int pieces) {
     return (pieces & ~(BAGUA_PIECES_COUNT_MASK | BAGUA_PIECES_TAPERED | BAGUA_PIECES_MULTIPATH)) == 0;
 }
 
+// Whether the op runs pipelined: every rank must decide alike (they would otherwise
+// post different collectives), so only values equal on every rank enter -- sizes,
+// dtype, p -- never this rank's pointer.  A rank whose tensor is not 16-B aligned
+// runs the same schedule on an aligned staging copy (with_aligned_copy).
 bool pipeline_fits(const BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, const Chunking& k) {
     const size_t esz = bagua_dtype_bytes(t->dtype);
     const size_t vec = t->dtype == BAGUA_DTYPE_F32 ? 4 : 8;  // payload bytes per 16-B vector
-    return k.p <= 16 && t->num_elem == t->num_elem_allocated && (k.S / k.p) % vec == 0 &&
-           (t->ptr + (uint64_t)k.rank * k.cs * esz) % 16 == 0 && c->t != nullptr;
+    return k.p <= 16 && t->num_elem == t->num_elem_allocated && (k.S / k.p) % vec == 0 && (k.cs * esz) % 16 == 0 &&
+           c->t != nullptr;
+}
+
+// Runs op(descriptors) on 16-B aligned copies of the tensors that are not aligned:
+// copied into one pool block on the op's stream first and back after the op (whose
+// work, side stream included, the stream has joined by then).  The aligned tensors
+// are passed as they are.
+template <typename F>
+int with_aligned_copy(BaguaSingleCommunicatorC* c, std::vector<const bagua_tensor_t*> ts, F&& op) {
+    size_t total = 0;
+    std::vector<size_t> off(ts.size(), 0);
+    for (size_t i = 0; i < ts.size(); ++i)
+        if (ts[i]->ptr % 16) {
+            off[i] = total;
+            total += (ts[i]->num_elem_allocated * bagua_dtype_bytes(ts[i]->dtype) + 255) / 256 * 256;
+        }
+    if (!total) return op(ts);
+    OpBuffer stage(c);
+    int rc = stage.allocate(c->device_id, total);
+    if (rc) return finish(c, rc);
+    std::vector<bagua_tensor_t> copies(ts.size());
+    std::vector<const bagua_tensor_t*> use(ts.size());
+    for (size_t i = 0; i < ts.size(); ++i) {
+        use[i] = ts[i];
+        if (!(ts[i]->ptr % 16)) continue;
+        copies[i] = *ts[i];
+        copies[i].ptr = stage.ptr() + off[i];
+        use[i] = &copies[i];
+        if (hipMemcpyAsync((void*)(uintptr_t)copies[i].ptr, (const void*)(uintptr_t)ts[i]->ptr,
+                           ts[i]->num_elem_allocated * bagua_dtype_bytes(ts[i]->dtype), hipMemcpyDeviceToDevice,
+                           c->stream) != hipSuccess)
+            return finish(c, BAGUA_ERR_HIP);
+    }
+    rc = op(use);
+    if (rc) return rc;  // the op finished (or enqueued) its own failure handling
+    for (size_t i = 0; i < ts.size(); ++i)
+        if (ts[i]->ptr % 16 &&
+            hipMemcpyAsync((void*)(uintptr_t)ts[i]->ptr, (const void*)(uintptr_t)use[i]->ptr,
+                           ts[i]->num_elem_allocated * bagua_dtype_bytes(ts[i]->dtype), hipMemcpyDeviceToDevice,
+                           c->stream) != hipSuccess)
+            return finish(c, BAGUA_ERR_HIP);
+    return finish(c, BAGUA_OK);
 }
 
 // bytes [lo, hi) of every segment that piece q of schedule `sched` covers: the header
@@ -392,6 +437,10 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
     pieces &= BAGUA_PIECES_COUNT_MASK;
     if (pieces < 1) pieces = k.p == 1 ? 1 : auto_pieces(k.cs);  // one rank: no exchange to hide
     if (pieces == 1 || !pipeline_fits(c, t, k)) return centralized(c, t, average, BAGUA_COMPRESSION_MINMAX_UINT8, true);
+    if (t->ptr % 16)
+        return with_aligned_copy(c, {t}, [&](const std::vector<const bagua_tensor_t*>& u) {
+            return centralized_pipelined(c, u[0], average, pieces | (caller & BAGUA_PIECES_TAPERED));
+        });
     const int sched = op_schedule(pieces, caller);
     DeviceGuard guard(c->device_id);
     if (c->ensure_side(4 * (size_t)pieces + 1)) return BAGUA_ERR_HIP;
@@ -753,6 +802,17 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
     const int n = (int)t->num_elem_allocated;
     const size_t S = bagua_compressed_size(method, t->dtype, 1, t->num_elem_allocated);
     if (!S) return BAGUA_ERR_UNSUPPORTED;
+    // fused kernels (csrc/kernels/decentralized.hip) for fully valid, same-shape
+    // MinMax buckets; anything else runs the reference's op sequence.  The choice (and
+    // with it the pipelined exchange schedule) depends only on values equal on every
+    // rank; a rank whose tensors are not 16-B aligned runs on aligned copies
+    bool fused = allow_fused && method == BAGUA_COMPRESSION_MINMAX_UINT8 && t->num_elem == t->num_elem_allocated;
+    for (const bagua_tensor_t* o : {weight, left, right})
+        fused = fused && o->dtype == t->dtype && o->num_elem == t->num_elem;
+    if (fused && (t->ptr % 16 || weight->ptr % 16 || left->ptr % 16 || right->ptr % 16))
+        return with_aligned_copy(c, {t, weight, left, right}, [&](const std::vector<const bagua_tensor_t*>& u) {
+            return decentralized(c, u[0], u[1], u[2], u[3], method, allow_fused, pieces);
+        });
     OpBuffer mine(c), lbuf(c), rbuf(c);
     TRY(mine.allocate(c->device_id, S));
     TRY(lbuf.allocate(c->device_id, S));
@@ -760,11 +820,6 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
     const bagua_tensor_t mv = u8_view(mine.ptr(), S, c->device_id);
     const bagua_tensor_t lv = u8_view(lbuf.ptr(), S, c->device_id);
     const bagua_tensor_t rv = u8_view(rbuf.ptr(), S, c->device_id);
-    // fused kernels (csrc/kernels/decentralized.hip) for fully valid, same-shape
-    // MinMax buckets; anything else runs the reference's op sequence
-    bool fused = allow_fused && method == BAGUA_COMPRESSION_MINMAX_UINT8 && t->num_elem == t->num_elem_allocated;
-    for (const bagua_tensor_t* o : {weight, left, right})
-        fused = fused && o->dtype == t->dtype && o->num_elem == t->num_elem;
     void* tp = (void*)(uintptr_t)t->ptr;
     void* wp = (void*)(uintptr_t)weight->ptr;
     void* lp = (void*)(uintptr_t)left->ptr;

@@ -356,3 +356,64 @@ def test_decentralized_multipath_multirank(bc, oracle_c, p, dtype, n, pieces, mu
     for k, wk in zip("twlr", want):
         for r in range(p):
             assert np.array_equal(host(dts[k][r], dtype).view(np.uint8), wk[r].view(np.uint8)), f"{k} rank {r}"
+
+
+@pytest.mark.parametrize("p,cs,pieces,offsets", [(4, 4096, 3, [0, 1, 0, 2]), (4, 999, 2, [0, 0, 0, 0]),
+                                                 (2, 40000, 2, [1, 0])])
+def test_pipelined_choice_is_rank_independent(bc, oracle_c, p, cs, pieces, offsets):
+    """Every rank must take the same op schedule (the collectives must match): the
+    pipelined/unpieced choice uses only sizes, never a rank's pointer.  A rank whose tensor
+    is misaligned (offsets, in elements) runs the pipelined schedule on an aligned copy;
+    a chunk size whose chunks are not 16-B aligned (cs = 999 f32) is unpieced on every
+    rank.  Centralized MinMax op with explicit pieces, every rank == the oracle."""
+    from bagua_core.communicator import loopback_communicators
+    rng = np.random.default_rng(cs + pieces)
+    xs = [(rng.standard_normal(p * cs) * 1e-3 + 0.01 * r).astype(np.float32) for r in range(p)]
+    want = simulate.centralized_low_precision(oracle_c, xs, F32, True)
+    comms = loopback_communicators(p, 0)
+    bufs = [torch.zeros(p * cs + off, device="cuda") for off in offsets]
+    ts = [b[off:] for b, off in zip(bufs, offsets)]
+    for t, x in zip(ts, xs):
+        t.copy_(torch.from_numpy(x))
+    torch.cuda.synchronize()
+    N = bc._native
+
+    def rank(r):
+        raw = bc.BaguaTensorPy(ts[r], f"g{r}").raw()
+        N.check(N.C.bagua_centralized_low_precision_pipelined(comms[r].handle, ctypes.byref(raw), 1,
+                                                              N.COMPRESSION_MINMAX_UINT8, pieces), f"rank {r}")
+
+    run_ranks(rank, p)
+    for r in range(p):
+        assert np.array_equal(host(ts[r], F32).view(np.uint8), want[r].view(np.uint8)), f"rank {r}"
+
+
+@pytest.mark.parametrize("offsets", [[0, 1], [1, 0, 0]])
+def test_ring_pipelined_with_a_misaligned_rank(bc, oracle_c, offsets):
+    """The pipelined ring op with one rank's tensors misaligned: that rank runs the fused,
+    pieced schedule on aligned copies, so every rank posts the same exchange groups."""
+    from bagua_core.communicator import loopback_communicators
+    p, n = len(offsets), 30011
+    rng = np.random.default_rng(77 + p)
+    arrs = {k: [(rng.standard_normal(n) * 1e-3).astype(np.float32) for _ in range(p)] for k in "twlr"}
+    want = simulate.decentralized_low_precision(oracle_c, arrs["t"], arrs["w"], arrs["l"], arrs["r"], F32)
+    comms = loopback_communicators(p, 0)
+
+    def place(a, off):
+        full = torch.zeros(n + off, device="cuda")
+        full[off:].copy_(torch.from_numpy(a))
+        return full[off:]
+
+    dts = {k: [place(a, off) for a, off in zip(arrs[k], offsets)] for k in "twlr"}
+    torch.cuda.synchronize()
+    N = bc._native
+
+    def rank(r):
+        raws = [bc.BaguaTensorPy(dts[k][r], k).raw() for k in "twlr"]
+        N.check(N.C.bagua_decentralized_low_precision_pipelined(comms[r].handle, *[ctypes.byref(x) for x in raws],
+                                                                N.COMPRESSION_MINMAX_UINT8, 3), f"rank {r}")
+
+    run_ranks(rank, p)
+    for k, wk in zip("twlr", want):
+        for r in range(p):
+            assert np.array_equal(host(dts[k][r], F32).view(np.uint8), wk[r].view(np.uint8)), f"{k} rank {r}"
