@@ -111,16 +111,19 @@ class BaguaTensorPy:
             return self._raw
         t = self._torch
         d = self._desc
+        ptr = t.data_ptr()
+        if ptr != d.ptr:
+            # new storage (a .data / set_ swap): re-read what may have changed with it --
+            # the bucket's native check (dtype and device may not change,
+            # datatypes/mod.rs:1079-1118) must see the device the storage is on now
+            dv = t.device
+            d.device_id = -1 if dv.type != "cuda" else (dv.index if dv.index is not None else d.device_id)
+            d.ptr = ptr
+        spec = _DTYPES.get(t.dtype)
+        d.dtype = spec[0] if spec else -1
         n = t.numel()
-        dev = t.device.index
-        if t.device.type != "cuda" or (dev is not None and dev != d.device_id):
-            # the bucket's native check (the device may not change, datatypes/mod.rs:1079-1118)
-            # must see the device the storage is on, not the one cached at construction
-            d.device_id = -1 if t.device.type != "cuda" else dev
-        d.ptr = t.data_ptr()
         d.num_elem = n
         d.num_elem_allocated = n
-        d.dtype = _DTYPES[t.dtype][0]
         return d
 
     # ---- accessors (lib.rs:280-298) -----------------------------------------

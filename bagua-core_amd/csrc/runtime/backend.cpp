@@ -174,8 +174,15 @@ int execute_bucket(BaguaBucketC* b, const std::vector<BucketTensor>& tensors, co
     if (tensors.empty()) return BAGUA_ERR_INVALID_ARG;
     const bagua_tensor_t& first = tensors[0].t;
     DeviceGuard guard(first.device_id);
-    for (uint64_t ev : events)  // :969-980 the stream waits for every tensor's ready event
+    // :969-980 the stream waits for every tensor's ready event -- unless it has already
+    // completed: a stream wait costs the queue a barrier packet (a few us between two
+    // buckets' kernels) even when there is nothing left to wait for
+    for (uint64_t ev : events) {
+        const hipError_t q = hipEventQuery((hipEvent_t)(uintptr_t)ev);
+        if (q == hipSuccess) continue;
+        if (q != hipErrorNotReady) (void)hipGetLastError();
         if (hipStreamWaitEvent(s, (hipEvent_t)(uintptr_t)ev, 0) != hipSuccess) return BAGUA_ERR_HIP;
+    }
     if (ops.empty()) return BAGUA_OK;
     hipStream_t os = ops_stream(ops);
     if (!os) os = s;
