@@ -36,6 +36,8 @@ constexpr int kPartialsSub = 8;
 constexpr int kPartialsBlocks = 1024;
 constexpr int kQuantBlocks = 8192;
 constexpr int kDequantBlocks = 16384;
+// the min/max pass reads non-temporally above this many MiB (partials_nt)
+constexpr int kPartialsNtAboveMiB = 1 << 20;  // effectively never, until measured (BAGUA_PARTIALS_NT A/B)
 
 __device__ __forceinline__ int64_t chunk_valid(int64_t in_num_elem, int64_t cs, int c) {
     // K:538-545: remaining elements, clamped to [0, chunk_size]
@@ -56,7 +58,9 @@ __device__ __forceinline__ void fold(float f, uint32_t& lo, uint32_t& hi) {
 // REV: the grid sweeps each chunk from its end to its start (min/max is
 // order-free), so what the Infinity Cache holds afterwards is the chunk's
 // beginning -- the piece the pipelined op quantises first
-template <typename T, bool REV = false>
+// NTL: non-temporal loads (no Infinity-Cache allocation; faster for a bucket larger
+// than the cache, tools/stream_probe.hip at 1 GiB: 6.7-6.8 vs 6.1-6.2 TB/s)
+template <typename T, bool REV = false, bool NTL = false>
 __global__ __launch_bounds__(kBlock) void minmax_partials_kernel(
     const typename T::storage* __restrict__ in, int64_t in_num_elem, int64_t cs, int target,
     uint2* __restrict__ partials) {
@@ -83,7 +87,10 @@ __global__ __launch_bounds__(kBlock) void minmax_partials_kernel(
         if (base + kBlock * SUB <= nvec) {  // full tile: SUB loads in flight per lane
             uint4 r[SUB];
 #pragma unroll
-            for (int k = 0; k < SUB; ++k) r[k] = vsrc[base + k * kBlock + threadIdx.x];  // default policy
+            for (int k = 0; k < SUB; ++k) {
+                if constexpr (NTL) r[k] = nt_load16(&vsrc[base + k * kBlock + threadIdx.x]);
+                else r[k] = vsrc[base + k * kBlock + threadIdx.x];  // default policy
+            }
 #pragma unroll
             for (int k = 0; k < SUB; ++k) {
                 float f[N];
@@ -438,6 +445,16 @@ int minmax_partials_blocks(int64_t cs, int per_vec, int nact, size_t ws_bytes) {
     return nblk > cap ? (int)cap : nblk;
 }
 
+// Load policy of the min/max pass: BAGUA_PARTIALS_NT=1 / 0 forces non-temporal /
+// default loads (A/B); unset: non-temporal when the pass reads more than the Infinity
+// Cache holds (nothing of it would still be there for the quantise pass anyway).
+template <typename T>
+static bool partials_nt(int64_t elems) {
+    const int env = tune_int("BAGUA_PARTIALS_NT", -1);
+    if (env >= 0) return env != 0;
+    return elems * (int64_t)sizeof(typename T::storage) > ((int64_t)kPartialsNtAboveMiB << 20);
+}
+
 // defined in minmax_resident.hip; BAGUA_ERR_UNSUPPORTED when the shape is not eligible
 template <typename T>
 int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, int p, uint8_t* out,
@@ -465,12 +482,24 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
         const int rc = resident_compress_impl<T>(input, in_num_elem, cs, p, out, (int64_t)out_bytes, target, s);
         if (rc != BAGUA_ERR_UNSUPPORTED) return rc;
     }
-    if ((stages & 1) && (stages & 4))
-        launch(minmax_partials_kernel<T, true>, dim3(nblk, nact), dim3(kBlock), 0, s,
-                           static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, partials);
-    else if (stages & 1)
-        launch(minmax_partials_kernel<T>, dim3(nblk, nact), dim3(kBlock), 0, s,
-                           static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, partials);
+    if (stages & 1) {
+        const bool rev = (stages & 4) != 0;
+        const bool nt = partials_nt<T>((int64_t)cs * nact);
+        const dim3 grid(nblk, nact);
+        const S* src = static_cast<const S*>(input);
+        if (rev && nt)
+            launch(minmax_partials_kernel<T, true, true>, grid, dim3(kBlock), 0, s, src, (int64_t)in_num_elem,
+                   (int64_t)cs, target, partials);
+        else if (rev)
+            launch(minmax_partials_kernel<T, true, false>, grid, dim3(kBlock), 0, s, src, (int64_t)in_num_elem,
+                   (int64_t)cs, target, partials);
+        else if (nt)
+            launch(minmax_partials_kernel<T, false, true>, grid, dim3(kBlock), 0, s, src, (int64_t)in_num_elem,
+                   (int64_t)cs, target, partials);
+        else
+            launch(minmax_partials_kernel<T, false, false>, grid, dim3(kBlock), 0, s, src, (int64_t)in_num_elem,
+                   (int64_t)cs, target, partials);
+    }
     if (stages & 2)
         launch((minmax_quantize_kernel<T, true>),
                dim3(blocks_for(e1 - e0, Vec<T>::N, nact, kSubtiles, tune_int("BAGUA_TUNE_QUANT_BLOCKS", kQuantBlocks)),
@@ -638,8 +667,12 @@ static int one_rank_impl(void* tensor, int num_elem, int average, void* ws, size
     const int nblk = ws ? minmax_partials_blocks(num_elem, Vec<T>::N, 1, ws_bytes) : 0;
     if (nblk < 1) return BAGUA_ERR_WORKSPACE;
     uint2* partials = static_cast<uint2*>(ws);
-    launch(minmax_partials_kernel<T>, dim3(nblk, 1), dim3(kBlock), 0, s, static_cast<const S*>(tensor),
-           (int64_t)num_elem, (int64_t)num_elem, -1, partials);
+    if (partials_nt<T>(num_elem))
+        launch(minmax_partials_kernel<T, false, true>, dim3(nblk, 1), dim3(kBlock), 0, s,
+               static_cast<const S*>(tensor), (int64_t)num_elem, (int64_t)num_elem, -1, partials);
+    else
+        launch(minmax_partials_kernel<T, false, false>, dim3(nblk, 1), dim3(kBlock), 0, s,
+               static_cast<const S*>(tensor), (int64_t)num_elem, (int64_t)num_elem, -1, partials);
     const dim3 grid(blocks_for(num_elem, Vec<T>::N, 1, kSubtiles, tune_int("BAGUA_TUNE_QUANT_BLOCKS", kQuantBlocks)),
                     1);
     if (average)

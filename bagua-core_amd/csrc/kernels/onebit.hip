@@ -614,11 +614,15 @@ static int ob_decompress_impl(const uint8_t* in, size_t in_bytes, int cs, int p,
     if (((uintptr_t)in + 32) % 4 || co % 4) return BAGUA_ERR_INVALID_ARG;
     const int64_t te = t_end < tiles ? t_end : tiles;
     if (te <= t_begin) return BAGUA_OK;
-    // default-policy stores: 43 us vs 50 us with nt stores per 256 MiB decode, and the
-    // next encode (nt loads) is unaffected (profiles/r01_decode_store_ab.jsonl).
-    // BAGUA_OB_DECODE_NT=1 / 0 forces nt / default stores (A/B at sizes past the
-    // Infinity Cache, where dirty lines cannot stay behind: tools/cache_state_probe.py)
-    const int nt = tune_int("BAGUA_OB_DECODE_NT", 0);
+    // Store policy by the bucket's size (all p chunks, not this launch's tile range):
+    // up to the 256 MiB Infinity Cache, default-policy stores (256 MiB f32: decode 42.6
+    // vs 47.8 us with nt stores, and the next encode unaffected,
+    // profiles/r04_onebit_decode_store_ab.jsonl); past it the cache cannot keep the
+    // dirty lines, which the next encode then writes back (1 GiB: encode 196 -> 186 us,
+    // decode 201 -> 194 us with nt stores, same file).  BAGUA_OB_DECODE_NT=1 / 0
+    // forces either (A/B).
+    const int env = tune_int("BAGUA_OB_DECODE_NT", -1);
+    const int nt = env >= 0 ? env : ((int64_t)cs * p * (int64_t)sizeof(S) > ((int64_t)256 << 20) ? 1 : 0);
     const dim3 grid(ob_blocks(te - t_begin, p, tune_int("BAGUA_TUNE_OB_DECODE_BLOCKS", kObDecodeBlocks)), p);
     if (nt == 1)
         launch(onebit_decode_kernel<T, true>, grid, dim3(kBlock), 0, s, in, co, (int64_t)cs, static_cast<S*>(out),
