@@ -36,8 +36,8 @@ constexpr int kPartialsSub = 8;
 constexpr int kPartialsBlocks = 1024;
 constexpr int kQuantBlocks = 8192;
 constexpr int kDequantBlocks = 16384;
-// the min/max pass reads non-temporally above this many MiB (partials_nt)
-constexpr int kPartialsNtAboveMiB = 1 << 20;  // effectively never, until measured (BAGUA_PARTIALS_NT A/B)
+// the pipelined op's min/max pass reads non-temporally above this many MiB (partials_nt)
+constexpr int kPartialsNtAboveMiB = 256;
 
 __device__ __forceinline__ int64_t chunk_valid(int64_t in_num_elem, int64_t cs, int c) {
     // K:538-545: remaining elements, clamped to [0, chunk_size]
@@ -446,13 +446,17 @@ int minmax_partials_blocks(int64_t cs, int per_vec, int nact, size_t ws_bytes) {
 }
 
 // Load policy of the min/max pass: BAGUA_PARTIALS_NT=1 / 0 forces non-temporal /
-// default loads (A/B); unset: non-temporal when the pass reads more than the Infinity
-// Cache holds (nothing of it would still be there for the quantise pass anyway).
+// default loads (A/B).  Unset: non-temporal for the pipelined op's backward pass (stage
+// 5) over more than the 256 MiB Infinity Cache -- a 1 GiB pass takes 154.8 instead of
+// 172.5 us (0.87 of 8 TB/s), the first quantise piece then misses the chunks' cached
+// beginnings (51 -> 57 us), a net 14 us off the op's unhidden prefix; everywhere else
+// the next kernel's cache hits are worth more (the one-rank op 0.519 vs 0.524 ms, 256 MiB
+// buckets 2,001 vs 1,860 GiB/s; profiles/r04_partials_nt_ab.jsonl).
 template <typename T>
-static bool partials_nt(int64_t elems) {
+static bool partials_nt(int64_t elems, bool rev) {
     const int env = tune_int("BAGUA_PARTIALS_NT", -1);
     if (env >= 0) return env != 0;
-    return elems * (int64_t)sizeof(typename T::storage) > ((int64_t)kPartialsNtAboveMiB << 20);
+    return rev && elems * (int64_t)sizeof(typename T::storage) > ((int64_t)kPartialsNtAboveMiB << 20);
 }
 
 // defined in minmax_resident.hip; BAGUA_ERR_UNSUPPORTED when the shape is not eligible
@@ -484,7 +488,7 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
     }
     if (stages & 1) {
         const bool rev = (stages & 4) != 0;
-        const bool nt = partials_nt<T>((int64_t)cs * nact);
+        const bool nt = partials_nt<T>((int64_t)cs * nact, rev);
         const dim3 grid(nblk, nact);
         const S* src = static_cast<const S*>(input);
         if (rev && nt)
@@ -667,7 +671,7 @@ static int one_rank_impl(void* tensor, int num_elem, int average, void* ws, size
     const int nblk = ws ? minmax_partials_blocks(num_elem, Vec<T>::N, 1, ws_bytes) : 0;
     if (nblk < 1) return BAGUA_ERR_WORKSPACE;
     uint2* partials = static_cast<uint2*>(ws);
-    if (partials_nt<T>(num_elem))
+    if (partials_nt<T>(num_elem, false))
         launch(minmax_partials_kernel<T, false, true>, dim3(nblk, 1), dim3(kBlock), 0, s,
                static_cast<const S*>(tensor), (int64_t)num_elem, (int64_t)num_elem, -1, partials);
     else

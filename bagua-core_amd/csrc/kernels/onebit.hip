@@ -591,12 +591,17 @@ static int ob_compress_impl(const void* input, int in_num_elem, int cs, int p, u
     const int64_t tb = stage == 2 ? 0 : t_begin, te = stage == 2 ? tiles : (t_end < tiles ? t_end : tiles);
     // nt loads: default-policy loads behind the decode's default-policy stores take
     // 77 us instead of 47 (profiles/r01_decode_store_ab.jsonl)
-    if (stage != 2 && te > tb)
-        launch(onebit_encode_kernel<T, sizeof(S) == 4 ? 1 : 2, true>,
-               dim3(ob_blocks(te - tb, nact, tune_int("BAGUA_TUNE_OB_ENCODE_BLOCKS", kObEncodeBlocks)), nact),
-               dim3(kBlock), 0, s,
-               static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, out, co, partials, tiles, tb,
-               te);
+    if (stage != 2 && te > tb) {
+        const dim3 grid(ob_blocks(te - tb, nact, tune_int("BAGUA_TUNE_OB_ENCODE_BLOCKS", kObEncodeBlocks)), nact);
+        // BAGUA_TUNE_OB_ENCODE_TPI=2: f32 tiles two per wave iteration (A/B; 16-bit types always take two)
+        if (sizeof(S) == 4 && tune_int("BAGUA_TUNE_OB_ENCODE_TPI", 1) == 2)
+            launch(onebit_encode_kernel<T, 2, true>, grid, dim3(kBlock), 0, s, static_cast<const S*>(input),
+                   (int64_t)in_num_elem, (int64_t)cs, target, out, co, partials, tiles, tb, te);
+        else
+            launch(onebit_encode_kernel<T, sizeof(S) == 4 ? 1 : 2, true>, grid, dim3(kBlock), 0, s,
+                   static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, target, out, co, partials, tiles,
+                   tb, te);
+    }
     if (stage != 1)
         launch(onebit_finalize_kernel, dim3(nact), dim3(kObFinalizeThreads), 0, s, partials, tiles,
                (int64_t)in_num_elem, (int64_t)cs, target, out, co, (int64_t)out_bytes, p);
