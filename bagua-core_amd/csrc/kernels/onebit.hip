@@ -31,9 +31,11 @@ constexpr int kObFinalizeThreads = 1024;
 // workgroups over 2048 (profiles/r01_onebit_shape_sweep.jsonl); round 3 found
 // one tile per wave better still (16384 workgroups for 2^26 f32 elements):
 // encode 45.8 -> 43.8 us, decode 42.7 -> 42.0 us per 256 MiB
-// (tools/grid_sweep.py, profiles/r03_grid_sweep.jsonl)
-constexpr int kObEncodeBlocks = 16384;
-constexpr int kObDecodeBlocks = 16384;
+// (tools/grid_sweep.py, profiles/r03_grid_sweep.jsonl); round 4 kept one tile per
+// wave up to 1 GiB buckets (65536 workgroups): 1 GiB encode 186 -> 176 us, decode
+// 193 -> 190 us, 256 MiB unchanged (profiles/r04_onebit_shape_sweep.jsonl)
+constexpr int kObEncodeBlocks = 65536;
+constexpr int kObDecodeBlocks = 65536;
 
 __device__ __forceinline__ int64_t ob_valid(int64_t in_num_elem, int64_t cs, int c) {
     int64_t r = in_num_elem - (int64_t)c * cs;
