@@ -410,3 +410,67 @@ def test_lanes_pipelined_op_buckets(bc, oracle_c, lanes):
                 host[r][b] = want[r]
                 assert np.array_equal(flats[r][b].cpu().numpy().view(np.uint32), want[r].view(np.uint32)), (it, b, r)
     del backends
+
+
+def test_lanes_mixed_ops_multirank(bc, oracle_c):
+    """Two lanes, p = 2 on the loopback transport, buckets alternating between the 1-bit
+    centralized op and the decentralized ring op (its weight/peer tensors per bucket):
+    every bucket on every rank equals the oracle's simulation, two iterations."""
+    from bagua_core.communicator import loopback_communicators
+    p, nb, n = 2, 4, 3 * 16384
+    comms = loopback_communicators(p, 0)
+    rng = np.random.default_rng(4711)
+    host = {(r, b, k): (rng.standard_normal(n) * 1e-3).astype(np.float32) for r in range(p) for b in range(nb)
+            for k in "twlr"}
+    dev = {key: torch.from_numpy(v.copy()).cuda() for key, v in host.items()}
+    backends, tensors = [], []
+    for r in range(p):
+        buckets, ts_r = [], []
+        for b in range(nb):
+            t = bc.BaguaTensorPy(dev[(r, b, "t")], f"g{b}")
+            bk = bc.BaguaBucketPy(f"bucket{b}", [t])
+            if b % 2 == 0:
+                bk.append_centralized_synchronous_op(comms[r], None, False, True, False, "OneBitSignScale")
+            else:
+                w, lft, rgt = (bc.BaguaTensorPy(dev[(r, b, k)], f"{k}{b}") for k in "wlr")
+                bk.append_low_precision_decentralized_synchronous_op(comms[r], None, False, "ring", "MinMaxUInt8",
+                                                                     w, lft, rgt)
+            buckets.append(bk)
+            ts_r.append(t)
+        be = bc.BaguaCommBackendPy(4, 0)
+        be.set_lanes(2)
+        be.register_ordered_buckets(buckets)
+        backends.append((be, buckets))
+        tensors.append(ts_r)
+    torch.cuda.synchronize()
+    for it in range(2):
+        want = {}
+        for b in range(nb):
+            if b % 2 == 0:
+                w = simulate.centralized_low_precision(oracle_c, [host[(r, b, "t")].copy() for r in range(p)], F32,
+                                                       True, method="OneBitSignScale")
+                for r in range(p):
+                    want[(r, b, "t")] = w[r]
+            else:
+                res = simulate.decentralized_low_precision(oracle_c, *[[host[(r, b, k)].copy() for r in range(p)]
+                                                                       for k in "twlr"], F32)
+                for k, wk in zip("twlr", res):
+                    for r in range(p):
+                        want[(r, b, k)] = wk[r]
+        done = [None] * p
+
+        def rank(r):
+            for b in reversed(range(nb)):
+                backends[r][0].mark_communication_ready(tensors[r][b], 0)
+            done[r] = backends[r][0].wait_pending_comm_ops()
+        ths = [threading.Thread(target=rank, args=(r,)) for r in range(p)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join(timeout=120)
+        assert done == [nb] * p, done
+        for key, w in want.items():
+            got = dev[key].cpu().numpy()
+            assert np.array_equal(got.view(np.uint32), w.view(np.uint32)), (it, key)
+            host[key] = w
+    del backends
