@@ -31,11 +31,14 @@ constexpr int kVecPerBlockTile = kBlock * kSubtiles;  // 1024 x 16-B vectors = 1
 // per CU; quantise and dequantise 4 per lane.  Round 3 (tools/grid_sweep.py,
 // profiles/r03_grid_sweep.jsonl): more, shorter workgroups let the dispatcher
 // balance the tail -- dequantise one tile per workgroup (16384 for 256 MiB f32:
-// 48.25 -> 47.75 us), quantise 32 per CU (51.0 -> 50.1 us).
+// 48.25 -> 47.75 us), quantise 32 per CU (51.0 -> 50.1 us).  Round 4 keeps the
+// dequantise at one tile per workgroup up to 1 GiB (65536: 214 -> 189.5 us per 1 GiB
+// decode, 256 MiB unchanged; 8192 stays best for the quantise;
+// profiles/r04_minmax_grid_sweep.jsonl).
 constexpr int kPartialsSub = 8;
 constexpr int kPartialsBlocks = 1024;
 constexpr int kQuantBlocks = 8192;
-constexpr int kDequantBlocks = 16384;
+constexpr int kDequantBlocks = 65536;
 // the pipelined op's min/max pass reads non-temporally above this many MiB (partials_nt)
 constexpr int kPartialsNtAboveMiB = 256;
 
