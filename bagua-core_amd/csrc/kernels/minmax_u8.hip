@@ -39,6 +39,8 @@ constexpr int kPartialsSub = 8;
 constexpr int kPartialsBlocks = 1024;
 constexpr int kQuantBlocks = 8192;
 constexpr int kDequantBlocks = 65536;
+// the one-rank op's table pass (read + write, like the dequantise)
+constexpr int kOneRankBlocks = 16384;  // 1 GiB op 0.524 -> 0.521 ms (profiles/r04_one_rank_grid_sweep.jsonl)
 // the pipelined op's min/max pass reads non-temporally above this many MiB (partials_nt)
 constexpr int kPartialsNtAboveMiB = 256;
 
@@ -680,8 +682,8 @@ static int one_rank_impl(void* tensor, int num_elem, int average, void* ws, size
     else
         launch(minmax_partials_kernel<T, false, false>, dim3(nblk, 1), dim3(kBlock), 0, s,
                static_cast<const S*>(tensor), (int64_t)num_elem, (int64_t)num_elem, -1, partials);
-    const dim3 grid(blocks_for(num_elem, Vec<T>::N, 1, kSubtiles, tune_int("BAGUA_TUNE_QUANT_BLOCKS", kQuantBlocks)),
-                    1);
+    const dim3 grid(
+        blocks_for(num_elem, Vec<T>::N, 1, kSubtiles, tune_int("BAGUA_TUNE_ONE_RANK_BLOCKS", kOneRankBlocks)), 1);
     if (average)
         launch(minmax_one_rank_kernel<T, 1>, grid, dim3(kBlock), 0, s, static_cast<S*>(tensor), (int64_t)num_elem,
                static_cast<const uint2*>(partials), nblk);
