@@ -63,6 +63,14 @@ def launch_ranks(world: int, argv: list, child_cmd: list | None = None) -> int:
     out = []
     reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
     reader.start()
+
+    def forward(signum, _frame):  # a launcher stopped by its caller stops its ranks too
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        sys.exit(128 + signum)
+
+    old_handlers = {sig: signal.signal(sig, forward) for sig in (signal.SIGTERM, signal.SIGINT)}
     rc = 0
     while True:
         codes = [p.poll() for p in procs]
@@ -85,6 +93,8 @@ def launch_ranks(world: int, argv: list, child_cmd: list | None = None) -> int:
                 p.wait()
         print(f"bench.py: a rank failed (exit {rc}); every rank stopped", file=sys.stderr, flush=True)
     reader.join(timeout=30)
+    for sig, h in old_handlers.items():
+        signal.signal(sig, h)
     if rc == 0:
         sys.stdout.write("".join(out))
         sys.stdout.flush()
