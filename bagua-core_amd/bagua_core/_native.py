@@ -26,6 +26,10 @@ for _p in (KERNELS_PATH, CORE_PATH):
 
 kernels = ctypes.CDLL(KERNELS_PATH, mode=ctypes.RTLD_GLOBAL)
 core = ctypes.CDLL(CORE_PATH, mode=ctypes.RTLD_GLOBAL)
+try:  # the per-tensor scheduler calls without ctypes (csrc/pyext/fastpath.c, links libbagua_core.so)
+    from . import _fastpath as FAST
+except ImportError as _e:
+    raise ImportError(f"bagua_core: the fast-path extension is missing; build it with `make -C {_PKG_ROOT}`") from _e
 
 # dtype / method / op codes (bagua_kernels.h, bagua_core.h)
 DTYPE_F32, DTYPE_F16, DTYPE_BF16, DTYPE_U8, DTYPE_I64, DTYPE_U64 = 0, 1, 2, 3, 4, 5

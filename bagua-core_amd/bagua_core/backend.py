@@ -18,7 +18,9 @@ import ctypes
 
 from . import _native as N
 from .bucket import BaguaBucketPy
-from .tensor import BaguaTensorPy
+from .tensor import _DTYPES, BaguaTensorPy
+
+_backend_mark = N.FAST.backend_mark
 
 
 class BaguaCommBackendPy:
@@ -28,12 +30,14 @@ class BaguaCommBackendPy:
         if not handle:
             raise RuntimeError(f"cannot create the comm backend on device {device_id}")
         self._handle = ctypes.c_void_p(handle)
+        self._h = int(handle)  # for the fast-path mark
         self._ordered: list[BaguaBucketPy] = []  # keeps the native buckets alive while registered
         self._names: set[str] = set()
 
     def __del__(self):
         h = getattr(self, "_handle", None)
         if h is not None and h.value:
+            self._h = 0
             N.C.bagua_comm_backend_destroy(h)
             self._handle = None
 
@@ -61,18 +65,30 @@ class BaguaCommBackendPy:
         self._names = {t.name() for b in buckets for t in b.tensors()}
 
     def mark_communication_ready(self, tensor: BaguaTensorPy, ready_cuda_event_ptr: int) -> None:
-        """lib.rs:300-319"""
+        """lib.rs:300-319.  The tensor's current storage goes with it (the reference reads
+        data_ptr / numel at run time, datatypes/mod.rs:775-791).  One call per gradient
+        tensor per step: the torch-backed case goes through the CPython fast path
+        (csrc/pyext/fastpath.c) with plain ints; errors are explained after the fact."""
+        t = tensor._torch
+        if t is not None:
+            ptr = t.data_ptr()
+            dev = tensor._mark_dev if ptr == tensor._mark_ptr else tensor._mark_device(ptr)
+            spec = _DTYPES.get(t.dtype)
+            rc = _backend_mark(self._h, tensor._name_b, ready_cuda_event_ptr or 0, ptr, t.numel(),
+                               spec[0] if spec else -1, dev)
+        else:
+            rc = N.C.bagua_comm_backend_mark_communication_ready_desc(
+                self._handle, tensor._name_b, int(ready_cuda_event_ptr or 0), ctypes.byref(tensor._raw))
+        if rc:
+            self._mark_failed(tensor, rc)
+
+    def _mark_failed(self, tensor: BaguaTensorPy, rc: int) -> None:
         if not self._ordered:
             raise RuntimeError("BackendError: ordered buckets not yet set in comm backend")
         name = tensor.name()
         if name not in self._names:
             raise RuntimeError(f"TensorError: tensor {name} is not registered in any bucket")
-        # the tensor's current storage goes with it (the reference reads data_ptr at run time)
-        rc = N.C.bagua_comm_backend_mark_communication_ready_desc(self._handle, name.encode(),
-                                                                 int(ready_cuda_event_ptr or 0),
-                                                                 ctypes.byref(tensor._current()))
-        if rc:
-            N.check(rc, "mark_communication_ready")
+        N.check(rc, "mark_communication_ready")
 
     def wait_pending_comm_ops(self) -> int:
         """lib.rs:321-337: wait for every scheduled op; returns how many finished."""

@@ -26,7 +26,7 @@ from typing import Callable, Optional
 
 from . import _native as N
 from .communicator import BaguaSingleCommunicatorPy
-from .tensor import BaguaTensorPy, compression_code
+from .tensor import _DTYPES, BaguaTensorPy, compression_code
 
 CALLBACK = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_char_p)
 
@@ -228,9 +228,17 @@ class BaguaBucketPy:
     # ---- readiness (datatypes/mod.rs:1256-1266, 793-813), by tensor name --------
     def mark_tensor_ready(self, tensor: BaguaTensorPy, ready_cuda_event_ptr: int = 0) -> None:
         # the tensor's CURRENT storage (data_ptr read at run time, datatypes/mod.rs:775-791)
-        N.check(N.C.bagua_bucket_mark_tensor_ready_desc(self._handle, tensor.name().encode(),
-                                                        int(ready_cuda_event_ptr), ctypes.byref(tensor._current())),
-                f"tensor {tensor.name()} is not in bucket {self.name} (or changed dtype/device)")
+        t = tensor._torch
+        if t is not None:
+            ptr = t.data_ptr()
+            dev = tensor._mark_dev if ptr == tensor._mark_ptr else tensor._mark_device(ptr)
+            spec = _DTYPES.get(t.dtype)
+            rc = N.FAST.bucket_mark(self._handle.value, tensor._name_b, int(ready_cuda_event_ptr or 0), ptr,
+                                    t.numel(), spec[0] if spec else -1, dev)
+        else:
+            rc = N.C.bagua_bucket_mark_tensor_ready_desc(self._handle, tensor._name_b, int(ready_cuda_event_ptr or 0),
+                                                         ctypes.byref(tensor._raw))
+        N.check(rc, f"tensor {tensor.name()} is not in bucket {self.name} (or changed dtype/device)")
 
     def _refresh(self) -> None:
         """re-read every tensor's storage (a .data / set_ swap after the bucket was built)"""

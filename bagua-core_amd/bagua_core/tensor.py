@@ -57,6 +57,7 @@ class BaguaTensorPy:
             raise RuntimeError("BaguaTensorPy requires a contiguous tensor")
         self._torch = torch_tensor
         self._name = name
+        self._name_b = name.encode()
         self._pool_ptr = 0
         self._raw = None
         self._streams: set[int] = set()
@@ -66,6 +67,8 @@ class BaguaTensorPy:
         self._desc.dtype = spec[0]
         self._desc.device_id = torch_tensor.device.index if torch_tensor.device.index is not None \
             else torch.cuda.current_device()
+        # the storage the scheduler's last mark saw and its device (_mark_device)
+        self._mark_ptr, self._mark_dev = -1, self._desc.device_id
 
     # ---- construction from a pool buffer (compress output) ------------------
     @classmethod
@@ -73,6 +76,7 @@ class BaguaTensorPy:
         obj = cls.__new__(cls)
         obj._torch = None
         obj._name = name
+        obj._name_b = name.encode()
         obj._raw = raw
         obj._pool_ptr = raw.ptr if owned else 0
         obj._streams = set()
@@ -125,6 +129,14 @@ class BaguaTensorPy:
         d.num_elem = n
         d.num_elem_allocated = n
         return d
+
+    def _mark_device(self, ptr: int) -> int:
+        """The device of the torch tensor's storage, re-read when a mark sees new storage
+        (`ptr`, a .data / set_ swap) and cached for the next marks."""
+        dv = self._torch.device
+        self._mark_dev = -1 if dv.type != "cuda" else (dv.index if dv.index is not None else self._desc.device_id)
+        self._mark_ptr = ptr
+        return self._mark_dev
 
     # ---- accessors (lib.rs:280-298) -----------------------------------------
     def name(self) -> str:

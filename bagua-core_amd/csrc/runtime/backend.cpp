@@ -63,15 +63,42 @@ struct BaguaBucketC {
     int sched_index = 0;  // position in the scheduler's registration order (its lane)
     std::vector<BucketTensor> tensors;
     std::vector<bagua_bucket_op_t> ops;
-    std::unordered_set<std::string> ready;  // tensor names marked ready (guarded by `mu`)
-    std::unordered_map<std::string, uint64_t> events;  // name -> ready event of the next execution
+    // readiness per tensor (guarded by `mu`): a mark is one hash lookup and a flag, and
+    // the readiness test a compare -- the reference's name set (datatypes/mod.rs:1256-1266)
+    // costs a walk over the bucket per mark
+    std::unordered_map<std::string, std::vector<int>> index;  // name -> tensor indices
+    std::vector<uint8_t> ready;       // tensor i marked since the last reset
+    std::vector<uint64_t> events;     // tensor i's ready event of the next execution (0: none)
+    std::vector<uint8_t> padding;     // "bagua_padding_tensor*": always counts as ready
+    int marked = 0, needed = 0;       // marked non-padding tensors / non-padding tensors
     std::mutex mu;
 
+    void init_index() {
+        const size_t n = tensors.size();
+        ready.assign(n, 0);
+        events.assign(n, 0);
+        padding.assign(n, 0);
+        marked = needed = 0;
+        for (size_t i = 0; i < n; ++i) {
+            index[tensors[i].name].push_back((int)i);
+            padding[i] = tensors[i].name.rfind("bagua_padding_tensor", 0) == 0;
+            needed += !padding[i];
+        }
+    }
+    void mark_locked(int i, uint64_t ev) {
+        if (!ready[i]) {
+            ready[i] = 1;
+            marked += !padding[i];
+        }
+        if (ev) events[i] = ev;
+    }
+    void reset_locked() {
+        std::fill(ready.begin(), ready.end(), 0);
+        marked = 0;
+    }
     bool ready_for_comm() {  // datatypes/mod.rs:1256-1266 (padding tensors count as ready)
         std::lock_guard<std::mutex> g(mu);
-        for (const BucketTensor& t : tensors)
-            if (!ready.count(t.name) && t.name.rfind("bagua_padding_tensor", 0) != 0) return false;
-        return true;
+        return marked == needed;
     }
 };
 
@@ -137,9 +164,10 @@ int run_op(const bagua_bucket_op_t& op, const bagua_tensor_t* flat, const char* 
 std::vector<uint64_t> take_events(BaguaBucketC* b) {
     std::lock_guard<std::mutex> g(b->mu);
     std::vector<uint64_t> ev;
-    for (auto& kv : b->events)  // one stream wait per distinct event (tensors often share one)
-        if (kv.second && std::find(ev.begin(), ev.end(), kv.second) == ev.end()) ev.push_back(kv.second);
-    b->events.clear();
+    for (uint64_t& e : b->events) {  // one stream wait per distinct event (tensors often share one)
+        if (e && std::find(ev.begin(), ev.end(), e) == ev.end()) ev.push_back(e);
+        e = 0;
+    }
     return ev;
 }
 
@@ -417,6 +445,7 @@ BaguaBucketC* bagua_bucket_create(const char* name, const bagua_tensor_t* tensor
     auto* b = new BaguaBucketC();
     b->name = name;
     for (int i = 0; i < n; ++i) b->tensors.push_back(BucketTensor{tensors[i], tensor_names[i]});
+    b->init_index();
     return b;
 }
 
@@ -468,23 +497,26 @@ int bagua_bucket_mark_tensor_ready_desc(BaguaBucketC* b, const char* tensor_name
                                         const bagua_tensor_t* current) {
     if (!b || !tensor_name) return BAGUA_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(b->mu);
-    for (BucketTensor& t : b->tensors)
-        if (t.name == tensor_name) {
-            const int rc = refresh_locked(t, current);
-            if (rc != BAGUA_OK) return rc;
-            b->ready.insert(t.name);
-            if (ready_event) b->events[t.name] = ready_event;
-            return BAGUA_OK;
-        }
-    return BAGUA_ERR_INVALID_ARG;
+    const auto it = b->index.find(tensor_name);
+    if (it == b->index.end()) return BAGUA_ERR_INVALID_ARG;
+    for (const int i : it->second) {
+        const int rc = refresh_locked(b->tensors[i], current);
+        if (rc != BAGUA_OK) return rc;
+        b->mark_locked(i, ready_event);
+    }
+    return BAGUA_OK;
 }
 
 int bagua_bucket_refresh_tensor(BaguaBucketC* b, const char* tensor_name, const bagua_tensor_t* current) {
     if (!b || !tensor_name || !current) return BAGUA_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(b->mu);
-    for (BucketTensor& t : b->tensors)
-        if (t.name == tensor_name) return refresh_locked(t, current);
-    return BAGUA_ERR_INVALID_ARG;
+    const auto it = b->index.find(tensor_name);
+    if (it == b->index.end()) return BAGUA_ERR_INVALID_ARG;
+    for (const int i : it->second) {
+        const int rc = refresh_locked(b->tensors[i], current);
+        if (rc != BAGUA_OK) return rc;
+    }
+    return BAGUA_OK;
 }
 
 int bagua_bucket_ready_for_comm(BaguaBucketC* b) { return b && b->ready_for_comm() ? 1 : 0; }
@@ -492,7 +524,7 @@ int bagua_bucket_ready_for_comm(BaguaBucketC* b) { return b && b->ready_for_comm
 int bagua_bucket_reset_comm_ready(BaguaBucketC* b) {
     if (!b) return BAGUA_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(b->mu);
-    b->ready.clear();
+    b->reset_locked();
     return BAGUA_OK;
 }
 

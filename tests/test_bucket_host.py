@@ -2,6 +2,7 @@
 fake device pointers -- the native bucket never dereferences them unless it
 executes.  Mirrors the reference's bucket lifecycle (datatypes/mod.rs:1072-1267,
 bagua-core-py/src/lib.rs:352-487)."""
+import ctypes
 import gc
 import weakref
 
@@ -61,3 +62,52 @@ def test_clear_ops_while_scheduled_keeps_ops_until_released():
     b.append_python_op(lambda name: None)
     b.clear_ops()
     assert b._retired == []
+
+
+def test_readiness_by_flags_through_the_fast_path():
+    """The native bucket's readiness (datatypes/mod.rs:1256-1266) through the CPython
+    fast path (csrc/pyext/fastpath.c): every non-padding tensor marked once makes the
+    bucket ready, repeated marks count once, padding tensors count as ready, an unknown
+    name or a dtype change is refused, and a reset starts over."""
+    import bagua_core as bc
+    from bagua_core import _native as N
+    names = ["w0", "bagua_padding_tensor_x", "w1", "w2"]
+    ts = [_tensor(bc, N, nm, 0x7f0000200000 + i * 8192) for i, nm in enumerate(names)]
+    b = bc.BaguaBucketPy("flags", ts)
+    h = b.handle.value
+
+    def mark(name, ev=0, dtype=N.DTYPE_F32, ptr=0x7f0000300000):
+        return N.FAST.bucket_mark(h, name.encode(), ev, ptr, 1024, dtype, 0)
+
+    for _ in range(2):
+        assert not b.ready_for_comm()
+        assert mark("w0", 11) == 0 and mark("w0", 12) == 0  # repeated: counted once
+        assert mark("w2") == 0
+        assert not b.ready_for_comm()
+        assert mark("nope") == N.STATUS_INVALID_ARG
+        assert mark("w1", dtype=N.DTYPE_F16) == N.STATUS_INVALID_ARG  # dtype may not change
+        assert not b.ready_for_comm()
+        assert mark("w1", 11) == 0
+        assert b.ready_for_comm()  # the padding tensor was never marked
+        b.reset_comm_ready()
+    # a refresh by an unknown name is refused too
+    assert N.C.bagua_bucket_refresh_tensor(b.handle, b"missing", ctypes.byref(ts[0]._raw)) == N.STATUS_INVALID_ARG
+    with pytest.raises(TypeError):
+        N.FAST.bucket_mark(h, b"w0", 0)
+
+
+def test_backend_mark_error_messages_without_a_gpu():
+    """mark_communication_ready's error path keeps the reference's messages
+    (lib.rs:300-319) while the call itself goes through the fast path."""
+    import bagua_core as bc
+    from bagua_core import _native as N
+    from bagua_core.backend import BaguaCommBackendPy
+    be = BaguaCommBackendPy.__new__(BaguaCommBackendPy)  # no native handle: the call returns an error
+    be._handle, be._h, be._ordered, be._names = ctypes.c_void_p(0), 0, [], set()
+    t = _tensor(bc, N, "g0", 0x7f0000400000)
+    with pytest.raises(RuntimeError, match="ordered buckets not yet set"):
+        be.mark_communication_ready(t, 0)
+    be._ordered = [object()]
+    with pytest.raises(RuntimeError, match="not registered in any bucket"):
+        be.mark_communication_ready(t, 0)
+    assert N.FAST.backend_mark(0, b"g0", 0, 1, 1, 0, 0) == N.STATUS_INVALID_ARG
