@@ -41,7 +41,8 @@ constexpr int kQuantBlocks = 8192;
 constexpr int kDequantBlocks = 65536;
 // the one-rank op's table pass (read + write, like the dequantise)
 constexpr int kOneRankBlocks = 16384;  // 1 GiB op 0.524 -> 0.521 ms (profiles/r04_one_rank_grid_sweep.jsonl)
-// the pipelined op's min/max pass reads non-temporally above this many MiB (partials_nt)
+// the Infinity Cache: min/max passes over larger buckets read non-temporally except
+// for the part the next kernel re-reads first (partials_nt, one_rank_impl)
 constexpr int kPartialsNtAboveMiB = 256;
 
 __device__ __forceinline__ int64_t chunk_valid(int64_t in_num_elem, int64_t cs, int c) {
@@ -64,11 +65,14 @@ __device__ __forceinline__ void fold(float f, uint32_t& lo, uint32_t& hi) {
 // order-free), so what the Infinity Cache holds afterwards is the chunk's
 // beginning -- the piece the pipelined op quantises first
 // NTL: non-temporal loads (no Infinity-Cache allocation; faster for a bucket larger
-// than the cache, tools/stream_probe.hip at 1 GiB: 6.7-6.8 vs 6.1-6.2 TB/s)
+// than the cache, tools/stream_probe.hip at 1 GiB: 6.7-6.8 vs 6.1-6.2 TB/s) for the
+// first `nt_until` vectors of each chunk's sweep; the tiles swept after them load with
+// the default policy, so the Infinity Cache keeps them for a pass that re-reads them
+// first (the sweep's end: a chunk's tail going forward, its beginning with REV)
 template <typename T, bool REV = false, bool NTL = false>
 __global__ __launch_bounds__(kBlock) void minmax_partials_kernel(
     const typename T::storage* __restrict__ in, int64_t in_num_elem, int64_t cs, int target,
-    uint2* __restrict__ partials) {
+    uint2* __restrict__ partials, int64_t nt_until) {
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
     const int c = target < 0 ? (int)blockIdx.y : target;
@@ -91,10 +95,12 @@ __global__ __launch_bounds__(kBlock) void minmax_partials_kernel(
         const int64_t base = REV ? (ntile - 1) * kBlock * SUB - fwd : fwd;
         if (base + kBlock * SUB <= nvec) {  // full tile: SUB loads in flight per lane
             uint4 r[SUB];
+            if (NTL && fwd + kBlock * SUB <= nt_until) {
 #pragma unroll
-            for (int k = 0; k < SUB; ++k) {
-                if constexpr (NTL) r[k] = nt_load16(&vsrc[base + k * kBlock + threadIdx.x]);
-                else r[k] = vsrc[base + k * kBlock + threadIdx.x];  // default policy
+                for (int k = 0; k < SUB; ++k) r[k] = nt_load16(&vsrc[base + k * kBlock + threadIdx.x]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < SUB; ++k) r[k] = vsrc[base + k * kBlock + threadIdx.x];  // default policy
             }
 #pragma unroll
             for (int k = 0; k < SUB; ++k) {
@@ -454,9 +460,11 @@ int minmax_partials_blocks(int64_t cs, int per_vec, int nact, size_t ws_bytes) {
 // default loads (A/B).  Unset: non-temporal for the pipelined op's backward pass (stage
 // 5) over more than the 256 MiB Infinity Cache -- a 1 GiB pass takes 154.8 instead of
 // 172.5 us (0.87 of 8 TB/s), the first quantise piece then misses the chunks' cached
-// beginnings (51 -> 57 us), a net 14 us off the op's unhidden prefix; everywhere else
-// the next kernel's cache hits are worth more (the one-rank op 0.519 vs 0.524 ms, 256 MiB
-// buckets 2,001 vs 1,860 GiB/s; profiles/r04_partials_nt_ab.jsonl).
+// beginnings (51 -> 57 us), a net 14 us off the op's unhidden prefix -- since kept
+// by loading the sweep's last 256 MiB with the default policy (compress_impl); elsewhere
+// the next kernel's cache hits are worth more (256 MiB buckets 2,001 vs 1,860 GiB/s;
+// profiles/r04_partials_nt_ab.jsonl); the one-rank op splits its pass the same way
+// (one_rank_impl).
 template <typename T>
 static bool partials_nt(int64_t elems, bool rev) {
     const int env = tune_int("BAGUA_PARTIALS_NT", -1);
@@ -496,18 +504,27 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
         const bool nt = partials_nt<T>((int64_t)cs * nact, rev);
         const dim3 grid(nblk, nact);
         const S* src = static_cast<const S*>(input);
+        // the last 256 MiB of the backward sweep, over all chunks, load with the default
+        // policy, so the chunks' beginnings -- the first quantise piece -- stay in the
+        // Infinity Cache (1 GiB, p = 1, 4 pieces: pass + piece 0 217 -> 208 us, piece 0
+        // 55 -> 49.5 us; profiles/r04_partials_keep_ab.jsonl); BAGUA_PARTIALS_KEEP_MIB
+        // overrides (0: every load non-temporal)
+        const int keep_mib = tune_int("BAGUA_PARTIALS_KEEP_MIB", kPartialsNtAboveMiB);
+        const int64_t chunk_bytes = (int64_t)cs * (int64_t)sizeof(S);
+        const int64_t keep = ((int64_t)keep_mib << 20) / nact;
+        const int64_t nt_until = keep > 0 ? (chunk_bytes > keep ? (chunk_bytes - keep) / 16 : 0) : INT64_MAX;
         if (rev && nt)
             launch(minmax_partials_kernel<T, true, true>, grid, dim3(kBlock), 0, s, src, (int64_t)in_num_elem,
-                   (int64_t)cs, target, partials);
+                   (int64_t)cs, target, partials, nt_until);
         else if (rev)
             launch(minmax_partials_kernel<T, true, false>, grid, dim3(kBlock), 0, s, src, (int64_t)in_num_elem,
-                   (int64_t)cs, target, partials);
+                   (int64_t)cs, target, partials, INT64_MAX);
         else if (nt)
             launch(minmax_partials_kernel<T, false, true>, grid, dim3(kBlock), 0, s, src, (int64_t)in_num_elem,
-                   (int64_t)cs, target, partials);
+                   (int64_t)cs, target, partials, INT64_MAX);
         else
             launch(minmax_partials_kernel<T, false, false>, grid, dim3(kBlock), 0, s, src, (int64_t)in_num_elem,
-                   (int64_t)cs, target, partials);
+                   (int64_t)cs, target, partials, INT64_MAX);
     }
     if (stages & 2)
         launch((minmax_quantize_kernel<T, true>),
@@ -676,12 +693,21 @@ static int one_rank_impl(void* tensor, int num_elem, int average, void* ws, size
     const int nblk = ws ? minmax_partials_blocks(num_elem, Vec<T>::N, 1, ws_bytes) : 0;
     if (nblk < 1) return BAGUA_ERR_WORKSPACE;
     uint2* partials = static_cast<uint2*>(ws);
-    if (partials_nt<T>(num_elem, false))
+    // the table pass sweeps backwards: the tail the min/max pass reads last is re-read
+    // first, from the Infinity Cache.  Above the cache size only the last 256 MiB load
+    // with the default policy, the rest non-temporally: 1 GiB op 0.503 -> 0.474 ms
+    // (sweep of the kept size 0..512 MiB: profiles/r04_one_rank_keep_probe*.jsonl);
+    // BAGUA_ONE_RANK_KEEP_MIB overrides (-1: every load with the default policy)
+    const int64_t bytes = (int64_t)num_elem * (int64_t)sizeof(S);
+    const int keep_mib = tune_int("BAGUA_ONE_RANK_KEEP_MIB", kPartialsNtAboveMiB);
+    const int64_t keep = keep_mib < 0 ? bytes : ((int64_t)keep_mib << 20);
+    if (keep < bytes)
         launch(minmax_partials_kernel<T, false, true>, dim3(nblk, 1), dim3(kBlock), 0, s,
-               static_cast<const S*>(tensor), (int64_t)num_elem, (int64_t)num_elem, -1, partials);
+               static_cast<const S*>(tensor), (int64_t)num_elem, (int64_t)num_elem, -1, partials,
+               (int64_t)((bytes - keep) / 16));
     else
         launch(minmax_partials_kernel<T, false, false>, dim3(nblk, 1), dim3(kBlock), 0, s,
-               static_cast<const S*>(tensor), (int64_t)num_elem, (int64_t)num_elem, -1, partials);
+               static_cast<const S*>(tensor), (int64_t)num_elem, (int64_t)num_elem, -1, partials, INT64_MAX);
     const dim3 grid(
         blocks_for(num_elem, Vec<T>::N, 1, kSubtiles, tune_int("BAGUA_TUNE_ONE_RANK_BLOCKS", kOneRankBlocks)), 1);
     if (average)

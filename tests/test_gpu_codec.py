@@ -554,3 +554,27 @@ def test_one_rank_op_matches_sequence(bc, oracle_c, dtype, case, offset):
         xt = to_dev(x, dtype, offset)
         assert K.bagua_minmax_u8_centralized_one_rank(dtype, xt.data_ptr(), n, average, ws.data_ptr(), wsb, None) == 0
         assert_float_bits_equal(to_host(xt, dtype), want, dtype, f"one rank {case} average={average}")
+
+
+@pytest.mark.parametrize("keep_mib", ["0", "1"])
+@pytest.mark.parametrize("dtype", [F32, BF16])
+def test_one_rank_op_load_policy_split(bc, oracle_c, dtype, keep_mib, monkeypatch):
+    """The one-rank op's min/max pass with non-temporal loads below the kept tail
+    (BAGUA_ONE_RANK_KEEP_MIB: all of it at 0, all but the last MiB at 1) gives the
+    same bits as the reference sequence: the load policy moves no value."""
+    from oracle import oracle_np as NP
+    from oracle import simulate
+    K = bc._native.K
+    monkeypatch.setenv("BAGUA_ONE_RANK_KEEP_MIB", keep_mib)
+    rng = np.random.default_rng(int(keep_mib) * 3 + dtype)
+    n = (3 << 20) + 4099
+    v = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+    v[n // 2] = 0.75  # the max inside the non-temporal part
+    v[n - 9] = -0.5   # the min inside the kept tail
+    x = NP.from_f32(v, dtype)
+    wsb = K.bagua_minmax_u8_workspace_bytes(n, 1)
+    ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+    want = simulate.centralized_low_precision(oracle_c, [x.copy()], dtype, True)[0]
+    xt = to_dev(x, dtype, 0)
+    assert K.bagua_minmax_u8_centralized_one_rank(dtype, xt.data_ptr(), n, 1, ws.data_ptr(), wsb, None) == 0
+    assert_float_bits_equal(to_host(xt, dtype), want, dtype, f"one rank keep={keep_mib}")
