@@ -302,7 +302,10 @@ struct Scheduled {
     std::vector<bagua_bucket_op_t> ops;    // the bucket's ops at scheduling time
     bool done = false;                     // executed (sync) / enqueued (async)
     int status = BAGUA_OK;
-    hipEvent_t finished = nullptr;         // async: recorded behind the bucket's work
+    // async: an event recorded on the bucket's stream behind its work, shared by every
+    // bucket the worker enqueued on that stream since the previous record (destroyed with
+    // the last of them)
+    std::shared_ptr<void> finished;
 };
 
 }  // namespace
@@ -322,19 +325,50 @@ struct BaguaCommBackendC {
     bool stop = false;
     bool async = true;                  // BAGUA_BACKEND_SYNC=1: every op waits for its stream
     int lanes = 2;                      // BAGUA_SCHED_LANES (async only; 1 = every bucket on the comm's stream)
-    std::vector<hipEvent_t> spare;      // completion events for reuse
     std::thread worker, monitor;
+    // async, worker thread only: buckets enqueued whose completion is not recorded yet,
+    // with their stream
+    std::vector<std::pair<std::shared_ptr<Scheduled>, hipStream_t>> uncovered;
 
-    hipEvent_t take_event() {  // caller holds mu
-        if (!spare.empty()) {
-            hipEvent_t e = spare.back();
-            spare.pop_back();
-            return e;
+    // Completion of the enqueued buckets: ONE event per stream behind all of them,
+    // recorded when the worker runs out of queued buckets.  A lane's stream runs its
+    // buckets in order, so the last record covers every earlier one, and a burst of
+    // buckets costs one record per lane instead of one per bucket (a record is ~3 us of
+    // worker time; the buckets are marked done -- wait_pending_comm_ops may look at them
+    // only once covered).
+    void cover_uncovered() {
+        if (uncovered.empty()) return;
+        std::vector<std::pair<hipStream_t, std::shared_ptr<void>>> recs;
+        for (const auto& u : uncovered) {
+            bool seen = false;
+            for (const auto& r : recs) seen = seen || r.first == u.second;
+            if (seen) continue;
+            hipEvent_t e = nullptr;
+            // completion only: no system-scope fence (profiles/r02_slot_event_ab.jsonl)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
+                e = nullptr;
+            if (e && hipEventRecord(e, u.second) != hipSuccess) {
+                (void)hipEventDestroy(e);
+                e = nullptr;
+            }
+            if (!e) (void)hipStreamSynchronize(u.second);  // nothing to wait on later: drain now
+            recs.emplace_back(u.second, e ? std::shared_ptr<void>(e, [](void* x) {
+                (void)hipEventDestroy((hipEvent_t)x);
+            }) : std::shared_ptr<void>());
         }
-        hipEvent_t e = nullptr;
-        // completion only: no system-scope fence (profiles/r02_slot_event_ab.jsonl)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) return nullptr;
-        return e;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            for (const auto& u : uncovered) {
+                for (const auto& r : recs)
+                    if (r.first == u.second) u.first->finished = r.second;
+                // also after a failed op: its bucket's earlier work may still be queued,
+                // and wait_pending_comm_ops must not return before it drained
+                if (!u.first->finished && u.first->status == BAGUA_OK) u.first->status = BAGUA_ERR_HIP;
+                u.first->done = true;
+            }
+        }
+        uncovered.clear();
+        cv_done.notify_all();
     }
 
     // BAGUA_SCHED_PROFILE=1: host time per bucket (waiting for work / execute_bucket /
@@ -365,8 +399,17 @@ struct BaguaCommBackendC {
             const clk::time_point t_wait = clk::now();
             {
                 std::unique_lock<std::mutex> lk(mu);
+                if (channel.empty() && !uncovered.empty()) {  // out of work: record completions
+                    lk.unlock();
+                    cover_uncovered();
+                    lk.lock();
+                }
                 cv_work.wait(lk, [&] { return stop || !channel.empty(); });
-                if (channel.empty()) return;  // stopping with nothing queued
+                if (channel.empty()) {  // stopping with nothing queued
+                    lk.unlock();
+                    cover_uncovered();
+                    return;
+                }
                 item = channel.front();
                 channel.pop_front();
                 cv_space.notify_all();
@@ -384,30 +427,24 @@ struct BaguaCommBackendC {
             hipStream_t s = ops_stream(ops);
             const int rc = execute_bucket(item->bucket, item->tensors, item->events, ops, s);
             const clk::time_point t_fin = clk::now();
-            hipEvent_t fin = nullptr;
+            bool idle = false;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                item->status = rc;
+                if (!async) item->done = true;
+                current.reset();
+                idle = channel.empty();
+            }
             if (async) {
-                // also after a failed op: its bucket's earlier work may still be queued, and
-                // wait_pending_comm_ops must not return before it drained
-                {
-                    std::lock_guard<std::mutex> lk(mu);
-                    fin = take_event();
-                }
-                if (fin && hipEventRecord(fin, s) != hipSuccess) fin = nullptr;
-                if (!fin && s) (void)hipStreamSynchronize(s);
+                uncovered.emplace_back(item, s);
+                if (idle) cover_uncovered();
+            } else {
+                cv_done.notify_all();
             }
             if (profile && prof.size() < (1u << 20)) {  // bounded: a measurement hook, not a log
                 prof.push_back({us(t_wait, t_exec), us(t_exec, t_fin), us(t_fin, clk::now())});
                 ++prof_n;
             }
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                item->status = rc;
-                item->finished = fin;
-                if (async && rc == BAGUA_OK && !fin) item->status = BAGUA_ERR_HIP;
-                item->done = true;
-                current.reset();
-            }
-            cv_done.notify_all();
         }
     }
 
@@ -564,7 +601,6 @@ void bagua_comm_backend_destroy(BaguaCommBackendC* be) {
     if (be->monitor.joinable()) be->monitor.join();
     int n = 0;
     (void)bagua_comm_backend_wait_pending_comm_ops(be, &n);
-    for (hipEvent_t e : be->spare) (void)hipEventDestroy(e);
     if (be->profile && be->prof_n)
         fprintf(stderr, "[bagua-core] scheduler: %zu buckets, host us per bucket (p50 / p90 / max of the second "
                         "half): waiting for work %.2f / %.2f / %.2f, execute_bucket %.2f / %.2f / %.2f, completion "
@@ -587,15 +623,21 @@ int bagua_comm_backend_wait_pending_comm_ops(BaguaCommBackendC* be, int* complet
         be->pending.clear();
         for (const auto& item : items) be->cv_done.wait(lk, [&] { return item->done; });
         lk.unlock();
+        // one synchronisation per distinct completion event (buckets share them)
+        std::vector<std::pair<void*, bool>> synced;
         for (const auto& item : items) {
-            if (!item->finished) continue;
-            const hipError_t e = hipEventSynchronize(item->finished);
-            if (e != hipSuccess && item->status == BAGUA_OK) item->status = BAGUA_ERR_HIP;
+            void* e = item->finished.get();
+            if (!e) continue;
+            bool seen = false;
+            for (const auto& x : synced) seen = seen || x.first == e;
+            if (!seen) synced.emplace_back(e, hipEventSynchronize((hipEvent_t)e) == hipSuccess);
         }
         lk.lock();
         for (const auto& item : items) {
-            if (item->finished) be->spare.push_back(item->finished);
-            item->finished = nullptr;
+            for (const auto& x : synced)
+                if (x.first == item->finished.get() && !x.second && item->status == BAGUA_OK)
+                    item->status = BAGUA_ERR_HIP;
+            item->finished.reset();
             ++n;
             if (rc == BAGUA_OK && item->status != BAGUA_OK) rc = item->status;
         }
