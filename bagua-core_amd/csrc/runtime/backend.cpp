@@ -391,8 +391,9 @@ struct BaguaCommBackendC {
         auto us = [](clk::time_point a, clk::time_point b) {
             return std::chrono::duration<double, std::micro>(b - a).count();
         };
-        // async: ops return once enqueued; buckets run back to back on the stream and
-        // wait_pending_comm_ops waits for each bucket's completion event
+        // async: ops return once enqueued; buckets run back to back on their lane's
+        // stream and wait_pending_comm_ops waits for the completion events covering them
+        // (cover_uncovered)
         g_async_ops = async;
         for (;;) {
             std::shared_ptr<Scheduled> item;

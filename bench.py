@@ -305,6 +305,13 @@ def bench_codec(args, onebit: bool = False):
     every = max(1, args.kernel_events_every)
     sampled = list(range(0, args.steps, every))
     ev = kernel_events(len(sampled))
+    resident = names[0] == "minmax_resident_encode_kernel"
+
+    def give_ups():  # one-launch encode workgroups that timed out in the exchange (synchronises sp)
+        c = ctypes.c_uint64(0)
+        N.check(K.bagua_minmax_u8_resident_give_ups(sp, ctypes.byref(c)), "resident give-ups")
+        return int(c.value)
+    gu0 = give_ups() if resident else 0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -316,6 +323,7 @@ def bench_codec(args, onebit: bool = False):
                 raise RuntimeError(f"kernel launch failed: {N.STATUS.get(rc, rc)}")
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    gu_timed = give_ups() - gu0 if resident else None
     ms = wall * 1e3 / args.steps
     value = esz * n / (ms * 1e-3) / GiB  # gradient bytes processed (4N fp32, 2N bf16)
     dom_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
@@ -340,6 +348,9 @@ def bench_codec(args, onebit: bool = False):
                           "frac": round(step_alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "per_kernel_note": "kernel-recorded HIP events (hipExtLaunchKernel); dominant kernel over the timed region "
                            f"(every {every}th step: {len(sampled)} of {args.steps}), others over the last warmup steps",
+        # workgroups of the one-launch encode that gave up waiting in its exchange over the
+        # timed steps (0 unless something else held CUs; each give-up re-reads its slices)
+        "resident_give_ups_timed": gu_timed,
         "encode_gib_s": round(esz * n / (sum(per[:-1]) * 1e-3) / GiB, 1),
         "decode_gib_s": round(esz * n / (per[-1] * 1e-3) / GiB, 1),
     }
