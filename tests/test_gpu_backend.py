@@ -474,3 +474,37 @@ def test_lanes_mixed_ops_multirank(bc, oracle_c):
             assert np.array_equal(got.view(np.uint32), w.view(np.uint32)), (it, key)
             host[key] = w
     del backends
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_completion_covers_every_bucket_of_a_burst(bc, comm, oracle_c, lanes):
+    """Buckets the worker enqueues in one burst share one completion event per lane
+    (backend.cpp cover_uncovered).  wait_pending_comm_ops must still return only after
+    every bucket's work finished: the ready event trails a long GPU sleep, so every lane
+    runs late, and the results are read right after the wait with no other
+    synchronisation.  A second burst (on the first one's output) works the same way."""
+    n_buckets, per = 5, 3 * 30000
+    host, parts, _keep = _grads(n_buckets, per, 11)
+    buckets, tensors = [], []
+    for b in range(n_buckets):
+        ts = [bc.BaguaTensorPy(t, f"c{b}.{i}") for i, t in enumerate(parts[b])]
+        bk = bc.BaguaBucketPy(f"cover{b}", ts)
+        bk.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+        buckets.append(bk)
+        tensors.append(ts)
+    backend = bc.BaguaCommBackendPy(8, 0)
+    backend.set_lanes(lanes)
+    backend.register_ordered_buckets(buckets)
+    want = host
+    for it in range(2):
+        want = [simulate.centralized_low_precision(oracle_c, [w], F32, True)[0] for w in want]
+        torch.cuda._sleep(50_000_000)  # the "backward pass" still running on the default stream
+        ev = torch.cuda.Event()
+        ev.record()
+        for b in range(n_buckets):
+            for t in tensors[b]:
+                backend.mark_communication_ready(t, ev.cuda_event)
+        assert backend.wait_pending_comm_ops() == n_buckets
+        for b in range(n_buckets):
+            got = torch.cat([t.reshape(-1) for t in parts[b]]).cpu().numpy()
+            assert np.array_equal(got.view(np.uint32), want[b].view(np.uint32)), f"iteration {it} bucket {b}"
