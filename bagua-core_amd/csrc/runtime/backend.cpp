@@ -16,7 +16,7 @@
 //   * wait_pending_comm_ops waits for every scheduled item (lib.rs:321-337);
 //   * a monitor logs an op that runs longer than 300 s (lib.rs:255-265; the
 //     reference panics the process, here the failure is logged and kept).
-//   * cross-bucket pipelining (async mode, BAGUA_SCHED_LANES, default 2): bucket
+//   * cross-bucket pipelining (async mode, BAGUA_SCHED_LANES, default 3): bucket
 //     i of the registration order runs its ops on lane 1 + i % lanes of its
 //     communicator -- a view with its own streams (comm_internal.hpp) -- so the
 //     next bucket's compress prefix and enqueue overlap this bucket's exchange and
@@ -324,7 +324,10 @@ struct BaguaCommBackendC {
     std::vector<std::string> failures;
     bool stop = false;
     bool async = true;                  // BAGUA_BACKEND_SYNC=1: every op waits for its stream
-    int lanes = 2;                      // BAGUA_SCHED_LANES (async only; 1 = every bucket on the comm's stream)
+    // BAGUA_SCHED_LANES (async only; 1 = every bucket on the comm's stream).  3: 32 x 25 MiB at
+    // one rank 1,521-1,582 GiB/s vs 1,373-1,475 with 2 and 1,380-1,419 with 4
+    // (profiles/r04_sched_lanes_sweep.jsonl)
+    int lanes = 3;
     std::thread worker, monitor;
     // async, worker thread only: buckets enqueued whose completion is not recorded yet,
     // with their stream

@@ -1100,7 +1100,7 @@ class SchedulerWorkload:
 def bench_backend(args, world: int, rank: int, local_rank: int):
     """The scheduler workload (SchedulerWorkload): `--buckets` x `--bucket-mib` MiB fp32
     buckets through the native scheduler, with cross-bucket lanes (backend.cpp; the
-    default 2) and, beside it, one lane (every bucket on the communicator's stream).
+    default 3) and, beside it, one lane (every bucket on the communicator's stream).
     value = GiB of gradient per second (all ranks)."""
     import torch.distributed as dist
     import bagua_core

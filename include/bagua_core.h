@@ -308,7 +308,7 @@ int bagua_comm_backend_failures(BaguaCommBackendC* backend);
 /* Cross-bucket pipelining (no reference counterpart): bucket i of the registration
  * order runs on lane 1 + i % lanes of its communicator -- a view with its own
  * streams -- so consecutive buckets overlap on the GPU; 1 = every bucket on the
- * communicator's stream (the reference's one stream).  Default 2 (BAGUA_SCHED_LANES),
+ * communicator's stream (the reference's one stream).  Default 3 (BAGUA_SCHED_LANES),
  * async schedulers only.  set_lanes first waits for everything scheduled;
  * bagua_comm_backend_lanes returns the lanes in effect. */
 int bagua_comm_backend_set_lanes(BaguaCommBackendC* backend, int lanes);
