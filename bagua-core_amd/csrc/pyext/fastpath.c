@@ -21,15 +21,25 @@ static int parse_mark(PyObject* const* args, Py_ssize_t nargs, void** handle, co
         PyErr_SetString(PyExc_TypeError, "expected (handle, name, event, ptr, num_elem, dtype, device_id)");
         return -1;
     }
+    /* each conversion is checked before the next: no C-API call runs with an error set */
     *handle = PyLong_AsVoidPtr(args[0]);
+    if (PyErr_Occurred()) return -1;
     *name = PyBytes_AsString(args[1]);
+    if (!*name) return -1;
     *event = (uint64_t)PyLong_AsUnsignedLongLongMask(args[2]);
+    if (PyErr_Occurred()) return -1;
     t->ptr = (uint64_t)PyLong_AsUnsignedLongLongMask(args[3]);
+    if (PyErr_Occurred()) return -1;
     t->num_elem = (uint64_t)PyLong_AsUnsignedLongLongMask(args[4]);
+    if (PyErr_Occurred()) return -1;
     t->num_elem_allocated = t->num_elem;
-    t->dtype = (int32_t)PyLong_AsLong(args[5]);
-    t->device_id = (int32_t)PyLong_AsLong(args[6]);
-    return PyErr_Occurred() ? -1 : 0;
+    const long dtype = PyLong_AsLong(args[5]);
+    if (dtype == -1 && PyErr_Occurred()) return -1;
+    const long device = PyLong_AsLong(args[6]);
+    if (device == -1 && PyErr_Occurred()) return -1;
+    t->dtype = (int32_t)dtype;
+    t->device_id = (int32_t)device;
+    return 0;
 }
 
 /* bagua_comm_backend_mark_communication_ready_desc */

@@ -508,3 +508,35 @@ def test_completion_covers_every_bucket_of_a_burst(bc, comm, oracle_c, lanes):
         for b in range(n_buckets):
             got = torch.cat([t.reshape(-1) for t in parts[b]]).cpu().numpy()
             assert np.array_equal(got.view(np.uint32), want[b].view(np.uint32)), f"iteration {it} bucket {b}"
+
+
+@pytest.mark.parametrize("dtype", [1, 2])  # F16 (a reference dtype), BF16 (extension)
+def test_scheduler_16bit_buckets_match_oracle(bc, comm, oracle_c, dtype):
+    """16-bit gradient buckets through the scheduler at the default lanes: every tensor
+    is marked through the fast path (csrc/pyext/fastpath.c) with its dtype code, and each
+    bucket ends bit-identical to the oracle's simulation of the reference op sequence
+    (centralized_low_precision_synchronous.rs:30-71 at one rank)."""
+    from oracle import oracle_np as NP
+    from test_gpu_multirank import dev, host
+    n_buckets, per = 4, 3 * 20000
+    rng = np.random.default_rng(40 + dtype)
+    xs = [NP.from_f32((rng.standard_normal(per) * 1e-2).astype(np.float32), dtype) for _ in range(n_buckets)]
+    flats = [dev(x, dtype) for x in xs]
+    buckets, tensors = [], []
+    for b, f in enumerate(flats):
+        ts = [bc.BaguaTensorPy(t, f"h{dtype}.{b}.{i}") for i, t in enumerate(f.view(3, -1).unbind(0))]
+        bk = bc.BaguaBucketPy(f"half{b}", ts)
+        bk.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+        buckets.append(bk)
+        tensors.append(ts)
+    backend = bc.BaguaCommBackendPy(4, 0)
+    backend.register_ordered_buckets(buckets)
+    ev = torch.cuda.Event()
+    ev.record()
+    for ts in tensors:
+        for t in ts:
+            backend.mark_communication_ready(t, ev.cuda_event)
+    assert backend.wait_pending_comm_ops() == n_buckets
+    for b in range(n_buckets):
+        want = simulate.centralized_low_precision(oracle_c, [xs[b].copy()], dtype, True)[0]
+        assert np.array_equal(host(flats[b], dtype).view(np.uint8), want.view(np.uint8)), f"bucket {b}"
