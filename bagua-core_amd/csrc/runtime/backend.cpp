@@ -303,8 +303,8 @@ struct Scheduled {
     bool done = false;                     // executed (sync) / enqueued (async)
     int status = BAGUA_OK;
     // async: an event recorded on the bucket's stream behind its work, shared by every
-    // bucket the worker enqueued on that stream since the previous record (destroyed with
-    // the last of them)
+    // bucket the worker enqueued on that stream since the previous record (back to the
+    // backend's pool with the last of them)
     std::shared_ptr<void> finished;
 };
 
@@ -332,6 +332,34 @@ struct BaguaCommBackendC {
     // async, worker thread only: buckets enqueued whose completion is not recorded yet,
     // with their stream
     std::vector<std::pair<std::shared_ptr<Scheduled>, hipStream_t>> uncovered;
+    // completion events for reuse: an event returns here when the last bucket sharing it
+    // is released by wait_pending_comm_ops (after its synchronisation); own mutex, never
+    // held while taking `mu`
+    std::mutex spare_mu;
+    std::vector<hipEvent_t> spare;
+
+    std::shared_ptr<void> completion_event(hipStream_t s) {
+        hipEvent_t e = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(spare_mu);
+            if (!spare.empty()) {
+                e = spare.back();
+                spare.pop_back();
+            }
+        }
+        // completion only: no system-scope fence (profiles/r02_slot_event_ab.jsonl)
+        if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
+            e = nullptr;
+        if (e && hipEventRecord(e, s) != hipSuccess) {
+            (void)hipEventDestroy(e);
+            e = nullptr;
+        }
+        if (!e) return nullptr;
+        return std::shared_ptr<void>(e, [this](void* x) {
+            std::lock_guard<std::mutex> lk(spare_mu);
+            spare.push_back((hipEvent_t)x);
+        });
+    }
 
     // Completion of the enqueued buckets: ONE event per stream behind all of them,
     // recorded when the worker runs out of queued buckets.  A lane's stream runs its
@@ -346,18 +374,9 @@ struct BaguaCommBackendC {
             bool seen = false;
             for (const auto& r : recs) seen = seen || r.first == u.second;
             if (seen) continue;
-            hipEvent_t e = nullptr;
-            // completion only: no system-scope fence (profiles/r02_slot_event_ab.jsonl)
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
-                e = nullptr;
-            if (e && hipEventRecord(e, u.second) != hipSuccess) {
-                (void)hipEventDestroy(e);
-                e = nullptr;
-            }
+            std::shared_ptr<void> e = completion_event(u.second);
             if (!e) (void)hipStreamSynchronize(u.second);  // nothing to wait on later: drain now
-            recs.emplace_back(u.second, e ? std::shared_ptr<void>(e, [](void* x) {
-                (void)hipEventDestroy((hipEvent_t)x);
-            }) : std::shared_ptr<void>());
+            recs.emplace_back(u.second, std::move(e));
         }
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -605,6 +624,7 @@ void bagua_comm_backend_destroy(BaguaCommBackendC* be) {
     if (be->monitor.joinable()) be->monitor.join();
     int n = 0;
     (void)bagua_comm_backend_wait_pending_comm_ops(be, &n);
+    for (hipEvent_t e : be->spare) (void)hipEventDestroy(e);
     if (be->profile && be->prof_n)
         fprintf(stderr, "[bagua-core] scheduler: %zu buckets, host us per bucket (p50 / p90 / max of the second "
                         "half): waiting for work %.2f / %.2f / %.2f, execute_bucket %.2f / %.2f / %.2f, completion "
