@@ -111,3 +111,23 @@ def test_backend_mark_error_messages_without_a_gpu():
     with pytest.raises(RuntimeError, match="not registered in any bucket"):
         be.mark_communication_ready(t, 0)
     assert N.FAST.backend_mark(0, b"g0", 0, 1, 1, 0, 0) == N.STATUS_INVALID_ARG
+
+
+def test_bucket_mark_tensor_ready_api_without_a_gpu():
+    """BaguaBucketPy.mark_tensor_ready (datatypes/mod.rs:793-813): marking every tensor
+    makes the bucket ready, a tensor of another bucket is refused with the bucket's name
+    in the message, and reset_comm_ready starts over."""
+    import bagua_core as bc
+    from bagua_core import _native as N
+    ts = [_tensor(bc, N, f"m{i}", 0x7f0000500000 + i * 8192) for i in range(3)]
+    b = bc.BaguaBucketPy("api", ts)
+    stranger = _tensor(bc, N, "elsewhere", 0x7f0000600000)
+    for _ in range(2):
+        for t in ts[:2]:
+            b.mark_tensor_ready(t)
+        assert not b.ready_for_comm()
+        with pytest.raises(RuntimeError, match="not in bucket api"):
+            b.mark_tensor_ready(stranger)
+        b.mark_tensor_ready(ts[2], 0)
+        assert b.ready_for_comm()
+        b.reset_comm_ready()
