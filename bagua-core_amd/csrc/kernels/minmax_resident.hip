@@ -255,9 +255,14 @@ __device__ void fold_missing_slices(const ResidentArgs& a, int cl, uint32_t tag,
     }
 }
 
-template <typename T, int BLOCK, int R, int H, int SB, bool NT>
+// NTM: non-temporal load mask -- bit 0: pass 2's re-reads of the streamed part;
+// bit 1: pass 1's loads of the part kept on chip (held in VGPRs / parked in LDS), which
+// nothing re-reads, so they need not take Infinity-Cache lines from the streamed part
+template <typename T, int BLOCK, int R, int H, int SB, int NTM>
 __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(ResidentArgs a) {
     constexpr int N = Vec<T>::N;
+    constexpr bool NT = (NTM & 1) != 0;
+    constexpr bool NT1 = (NTM & 2) != 0;
     constexpr int W = BLOCK / kWave;
     // dynamic LDS only (guide Guideline 17): [H * BLOCK parked vectors][scratch]
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
@@ -296,7 +301,7 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             const int64_t i = v0 + (int64_t)k * BLOCK + t;
-            held[k] = v[i < vl ? i : vl];
+            held[k] = NT1 ? nt_load16(&v[i < vl ? i : vl]) : v[i < vl ? i : vl];
         }
         // software-pipelined: the next batch of parked vectors is in flight while the
         // current one (first: the held vectors) is folded, so memory never waits on VALU
@@ -305,7 +310,7 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
         for (int j = 0; j < SB; ++j) {
             if (j < H) {
                 const int64_t i = v0 + (int64_t)(R + j) * BLOCK + t;
-                cur[j] = v[i < vl ? i : vl];
+                cur[j] = NT1 ? nt_load16(&v[i < vl ? i : vl]) : v[i < vl ? i : vl];
             }
         }
 #pragma unroll
@@ -316,7 +321,7 @@ __global__ __launch_bounds__(BLOCK, 1) void minmax_resident_encode_kernel(Reside
             for (int j = 0; j < SB; ++j) {
                 if (kb + SB + j < H) {
                     const int64_t i = v0 + (int64_t)(R + kb + SB + j) * BLOCK + t;
-                    nxt[j] = v[i < vl ? i : vl];
+                    nxt[j] = NT1 ? nt_load16(&v[i < vl ? i : vl]) : v[i < vl ? i : vl];
                 }
             }
 #pragma unroll
@@ -539,24 +544,32 @@ static ResidentDevice g_res_dev[64];
 // kernel configurations: {BLOCK, R vectors per lane in VGPRs, H per lane in LDS, SB stream batch}
 struct ResidentCfg {
     int block, r, h, sb;
-    bool nt;  // pass-2 re-reads non-temporal
+    int ntm;  // non-temporal loads: bit 0 pass-2 re-reads, bit 1 pass-1 loads of the on-chip part
 };
 static constexpr ResidentCfg kResCfg[] = {
-    {256, 32, 39, 8, false},   // 0
-    {256, 48, 39, 8, false},   // 1
-    {512, 24, 19, 8, false},   // 2
-    {256, 0, 0, 8, false},     // 3: no retention (Infinity Cache only)
-    {256, 32, 0, 8, false},    // 4: VGPRs only
-    {256, 16, 39, 16, false},  // 5
-    {256, 64, 39, 8, false},   // 6
-    {256, 80, 39, 8, false},   // 7
-    {256, 72, 39, 8, false},   // 8
-    {512, 28, 19, 8, false},   // 9
-    {256, 80, 39, 8, true},    // 10
-    {512, 28, 19, 8, true},    // 11
+    {256, 32, 39, 8, 0},   // 0
+    {256, 48, 39, 8, 0},   // 1
+    {512, 24, 19, 8, 0},   // 2
+    {256, 0, 0, 8, 0},     // 3: no retention (Infinity Cache only)
+    {256, 32, 0, 8, 0},    // 4: VGPRs only
+    {256, 16, 39, 16, 0},  // 5
+    {256, 64, 39, 8, 0},   // 6
+    {256, 80, 39, 8, 0},   // 7
+    {256, 72, 39, 8, 0},   // 8
+    {512, 28, 19, 8, 0},   // 9
+    {256, 80, 39, 8, 1},    // 10
+    {512, 28, 19, 8, 1},       // 11
+    {512, 28, 19, 8, 3},       // 12: 11 + the on-chip part loaded non-temporally
+    {512, 28, 19, 8, 2},       // 13: only the on-chip part non-temporal
 };
 constexpr int kResNumCfg = (int)(sizeof(kResCfg) / sizeof(kResCfg[0]));
-constexpr int kResDefaultCfg = 11;  // fastest config-2 step (tools/resident_sweep.sh)
+// 12: config 11 with the on-chip part of pass 1 also loaded non-temporally.  The
+// one-bucket loop is unchanged (1,894-1,898 vs 1,892-1,916 GiB/s), and alternating
+// buckets -- a bucket last touched a whole other bucket ago, as in training -- gain
+// 1,900-1,928 vs 1,849-1,886 GiB/s (profiles/r04_resident_ntm_ab.jsonl; 13, the
+// on-chip part non-temporal with default re-reads, shortens the encode to 78-80 us
+// but slows the decode after it by as much)
+constexpr int kResDefaultCfg = 12;
 
 static size_t resident_lds_bytes(const ResidentCfg& c) {
     return (size_t)c.h * c.block * 16 + 16 * ((2 * (c.block / kWave) + 4 + 3) / 4);
@@ -565,7 +578,7 @@ static size_t resident_lds_bytes(const ResidentCfg& c) {
 template <typename T, int CFG>
 static void* resident_kernel_ptr() {
     constexpr ResidentCfg c = kResCfg[CFG];
-    return reinterpret_cast<void*>(&minmax_resident_encode_kernel<T, c.block, c.r, c.h, c.sb, c.nt>);
+    return reinterpret_cast<void*>(&minmax_resident_encode_kernel<T, c.block, c.r, c.h, c.sb, c.ntm>);
 }
 
 template <typename T>
@@ -583,6 +596,8 @@ static void* resident_kernel_for(int cfg) {
         case 9: return resident_kernel_ptr<T, 9>();
         case 10: return resident_kernel_ptr<T, 10>();
         case 11: return resident_kernel_ptr<T, 11>();
+        case 12: return resident_kernel_ptr<T, 12>();
+        case 13: return resident_kernel_ptr<T, 13>();
     }
     return nullptr;
 }
@@ -805,7 +820,7 @@ int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, i
 #define BAGUA_RES_LAUNCH(I)                                                                                 \
     case I: {                                                                                               \
         constexpr ResidentCfg k = kResCfg[I];                                                               \
-        launch(minmax_resident_encode_kernel<T, k.block, k.r, k.h, k.sb, k.nt>, dim3(a.grid), dim3(k.block),      \
+        launch(minmax_resident_encode_kernel<T, k.block, k.r, k.h, k.sb, k.ntm>, dim3(a.grid), dim3(k.block),     \
                (uint32_t)pl.lds, s, a);                                                                     \
         break;                                                                                              \
     }
@@ -821,6 +836,8 @@ int resident_compress_impl(const void* input, int64_t in_num_elem, int64_t cs, i
         BAGUA_RES_LAUNCH(9)
         BAGUA_RES_LAUNCH(10)
         BAGUA_RES_LAUNCH(11)
+        BAGUA_RES_LAUNCH(12)
+        BAGUA_RES_LAUNCH(13)
 #undef BAGUA_RES_LAUNCH
         default:
             return BAGUA_ERR_UNSUPPORTED;  // a configuration without a launch: never silently skip the encode
