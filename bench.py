@@ -1172,7 +1172,10 @@ def main():
         del xb, cb
         if args.workload == "auto" and world == 1 and not args.no_allreduce_p1 and not args.elements:
             # the default line: config 2 (headline) + config 4 at one rank (the 1 -> 8 GPU curve's N = 1 point)
-            extra["allreduce_p1"] = allreduce_p1(args)
+            try:
+                extra["allreduce_p1"] = allreduce_p1(args)
+            except Exception as e:  # noqa: BLE001 - a failed side measurement must not lose the headline line
+                extra["allreduce_p1"] = {"error": str(e)[:200]}
         dtype = f"{args.dtype} -> u8" if workload == "codec" else f"{args.dtype} -> 1bit"
     elif workload == "host":
         value, ms, roof, cfg, extra, (xb, cb) = bench_host(args)
