@@ -1168,7 +1168,10 @@ def main():
     if workload in ("codec", "onebit"):
         value, ms, roof, cfg, extra, (xb, cb) = bench_codec(args, onebit=(workload == "onebit"))
         if rank == 0 and not args.no_cpu_baseline:
-            cpu = cpu_codec_baseline(args, xb, cb, onebit=(workload == "onebit"))
+            try:
+                cpu = cpu_codec_baseline(args, xb, cb, onebit=(workload == "onebit"))
+            except Exception as e:  # noqa: BLE001 - a failed baseline must not lose the headline line
+                cpu = {"error": str(e)[:200]}
         del xb, cb
         if args.workload == "auto" and world == 1 and not args.no_allreduce_p1 and not args.elements:
             # the default line: config 2 (headline) + config 4 at one rank (the 1 -> 8 GPU curve's N = 1 point)
@@ -1180,7 +1183,10 @@ def main():
     elif workload == "host":
         value, ms, roof, cfg, extra, (xb, cb) = bench_host(args)
         if rank == 0 and not args.no_cpu_baseline:
-            cpu = cpu_codec_baseline(args, xb, cb)
+            try:
+                cpu = cpu_codec_baseline(args, xb, cb)
+            except Exception as e:  # noqa: BLE001 - a failed baseline must not lose the headline line
+                cpu = {"error": str(e)[:200]}
         del xb, cb
         dtype = "f32 -> u8"
     else:
