@@ -89,6 +89,8 @@ KERNEL_SIGNATURES = {
     "bagua_minmax_u8_release_stream": (_i32, [_vp]),
     "bagua_minmax_u8_set_stream_resident": (_i32, [_vp, _i32]),
     "bagua_minmax_u8_centralized_one_rank": (_i32, [_i32, _vp, _i32, _i32, _vp, _sz, _vp]),
+    "bagua_onebit_one_rank_workspace_bytes": (_sz, [_i32]),
+    "bagua_onebit_centralized_one_rank": (_i32, [_i32, _vp, _i32, _i32, _vp, _sz, _vp]),
     "bagua_minmax_u8_resident_slots_in_use": (_i32, [_i32]),
     "bagua_minmax_u8_resident_give_ups": (_i32, [_vp, ctypes.POINTER(_u64)]),
     "bagua_minmax_u8_decompress_reduce": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _vp]),
@@ -227,6 +229,9 @@ CORE_SIGNATURES = {
     "bagua_comm_backend_mark_communication_ready_desc": (_i32, [_vp, ctypes.c_char_p, _u64, _T]),
     "bagua_comm_backend_wait_pending_comm_ops": (_i32, [_vp, ctypes.POINTER(_i32)]),
     "bagua_comm_backend_failures": (_i32, [_vp]),
+    "bagua_comm_schedule_config": (_i32, [_vp, ctypes.POINTER(ctypes.c_int32), _i32]),
+    "bagua_comm_backend_failure_message": (_i32, [_vp, _i32, ctypes.c_char_p, _sz]),
+    "bagua_comm_backend_set_op_timeout_ms": (_i32, [_vp, ctypes.c_int64]),
     "bagua_comm_backend_set_lanes": (_i32, [_vp, _i32]),
     "bagua_comm_backend_lanes": (_i32, [_vp]),
     "bagua_ring_exchange_ops": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),

@@ -8,8 +8,10 @@ and while the FRONT bucket is fully ready it is rotated to the back and
 scheduled on a bounded channel to one native worker thread, which makes the
 communicator stream wait for the tensors' ready events and runs the bucket's
 ops; `wait_pending_comm_ops()` blocks until every scheduled bucket finished and
-returns how many.  A native monitor flags an op running longer than 300 s
-(lib.rs:255-265; logged and counted instead of panicking the process).  Every
+returns how many.  A native monitor fails an op still running 300 s after the
+worker picked it up (lib.rs:255-265): it aborts the op's communicators and
+wait_pending_comm_ops raises with the monitor's message, where the reference
+panics the process.  Every
 call releases the GIL (ctypes), so buckets communicate while Python computes.
 """
 from __future__ import annotations
@@ -97,7 +99,9 @@ class BaguaCommBackendPy:
         for b in self._ordered:  # nothing scheduled is left to run: cleared ops may go now
             b._release_retired()
         if rc:
-            raise RuntimeError(f"comm op failed: {N.STATUS.get(rc, rc)} ({n.value} ops waited for)")
+            why = "; ".join(self.failures())
+            raise RuntimeError(f"comm op failed: {N.STATUS.get(rc, rc)} ({n.value} ops waited for)"
+                               + (f": {why}" if why else ""))
         return n.value
 
     def _holds(self, bucket: BaguaBucketPy) -> bool:
@@ -112,6 +116,18 @@ class BaguaCommBackendPy:
     def lanes(self) -> int:
         return int(N.C.bagua_comm_backend_lanes(self._handle))
 
+    def set_op_timeout(self, seconds: float) -> None:
+        """the monitor's limit (default 300 s, lib.rs:255-265; BAGUA_COMM_OP_TIMEOUT_S): an op
+        still running that long after the worker picked it up is failed and its
+        communicators are aborted, so wait_pending_comm_ops raises instead of hanging"""
+        N.check(N.C.bagua_comm_backend_set_op_timeout_ms(self._handle, max(1, int(seconds * 1000))),
+                "set_op_timeout")
+
     def failures(self) -> list[str]:
-        """ops the monitor saw running longer than 300 s"""
-        return ["comm op has not finished for 5 min"] * max(0, N.C.bagua_comm_backend_failures(self._handle))
+        """the monitor's messages, one per op it failed"""
+        out = []
+        buf = ctypes.create_string_buffer(512)
+        for i in range(max(0, N.C.bagua_comm_backend_failures(self._handle))):
+            if N.C.bagua_comm_backend_failure_message(self._handle, i, buf, len(buf)) >= 0:
+                out.append(buf.value.decode(errors="replace"))
+        return out

@@ -68,6 +68,12 @@ class BaguaSingleCommunicatorPy:
     def check_abort(self) -> bool:
         return bool(N.C.bagua_comm_check_abort(self._handle))
 
+    def schedule_config(self) -> dict:
+        """the schedule switches fixed at creation, equal on every rank (bagua_core.h)"""
+        out = (ctypes.c_int32 * 5)()
+        N.check(N.C.bagua_comm_schedule_config(self._handle, out, 5), "schedule_config")
+        return dict(zip(("pieces_cap", "min_piece", "taper", "multipath", "check"), out))
+
     # ---- collectives (communicators/mod.rs:473-1043) --------------------------
     def _call(self, fn, what, *tensors, extra=()):
         raws = [t.raw() for t in tensors]

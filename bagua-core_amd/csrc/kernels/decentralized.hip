@@ -200,14 +200,7 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
                                                             int64_t e0, int64_t e1) {
     // elements [e0, e1) (e0 a multiple of N; e1 too unless it is n)
     constexpr int N = Vec<T>::N;
-    const QParams qm = read_header<T>(mine), ql = read_header<T>(from_left), qr = read_header<T>(from_right);
-    // per-byte dequantised values of the three buffers (codec_common.hpp "dequantisation tables")
-    static_assert(kBlock == 256, "one table entry per thread");
     __shared__ float tm[256], tl[256], tr[256];
-    tm[threadIdx.x] = as_stored<T>(dequant(threadIdx.x, qm));
-    tl[threadIdx.x] = as_stored<T>(dequant(threadIdx.x, ql));
-    tr[threadIdx.x] = as_stored<T>(dequant(threadIdx.x, qr));
-    __syncthreads();
     const uint8_t* pm = mine + 32;
     const uint8_t* pl = from_left + 32;
     const uint8_t* pr = from_right + 32;
@@ -243,21 +236,42 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
     };
     // U vectors per tensor per iteration (k-th at offset k * kstep), all loads
     // issued before any is consumed
-    auto batch = [&](int64_t v, int64_t kstep) {
+    struct Regs {
         uint32_t bm[U][N], bl[U][N], br[U][N];
         uint4 rl[U], rr[U], rw[U];
+    };
+    auto load_batch = [&](int64_t v, int64_t kstep, Regs& g) {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             const int64_t u = v + k * kstep;
-            load_bytes<T>(pm + u * N, bm[k]);
-            load_bytes<T>(pl + u * N, bl[k]);
-            load_bytes<T>(pr + u * N, br[k]);
-            rl[k] = load16<NTL>(l4 + u);
-            rr[k] = load16<NTL>(r4 + u);
-            rw[k] = load16<NTL>(w4 + u);
+            load_bytes<T>(pm + u * N, g.bm[k]);
+            load_bytes<T>(pl + u * N, g.bl[k]);
+            load_bytes<T>(pr + u * N, g.br[k]);
+            g.rl[k] = load16<NTL>(l4 + u);
+            g.rr[k] = load16<NTL>(r4 + u);
+            g.rw[k] = load16<NTL>(w4 + u);
         }
+    };
+    auto use_batch = [&](int64_t v, int64_t kstep, const Regs& g) {
 #pragma unroll
-        for (int k = 0; k < U; ++k) body(v + k * kstep, bm[k], bl[k], br[k], rl[k], rr[k], rw[k]);
+        for (int k = 0; k < U; ++k) body(v + k * kstep, g.bm[k], g.bl[k], g.br[k], g.rl[k], g.rr[k], g.rw[k]);
+    };
+    auto batch = [&](int64_t v, int64_t kstep) {
+        Regs g;
+        load_batch(v, kstep, g);
+        use_batch(v, kstep, g);
+    };
+    // per-byte dequantised values of the three buffers (codec_common.hpp "dequantisation
+    // tables"), built after the first batch's loads are out: with one tile per workgroup
+    // (the default shape) the header reads and the barrier were otherwise the whole
+    // prologue of every workgroup, with no HBM request in flight
+    auto tables = [&]() {
+        const QParams qm = read_header<T>(mine), ql = read_header<T>(from_left), qr = read_header<T>(from_right);
+        static_assert(kBlock == 256, "one table entry per thread");
+        tm[threadIdx.x] = as_stored<T>(dequant(threadIdx.x, qm));
+        tl[threadIdx.x] = as_stored<T>(dequant(threadIdx.x, ql));
+        tr[threadIdx.x] = as_stored<T>(dequant(threadIdx.x, qr));
+        __syncthreads();
     };
     if constexpr (CONTIG) {
         const int64_t tile = (int64_t)U * kBlock;
@@ -266,9 +280,19 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
         const int64_t lo = vb + (int64_t)blockIdx.x * per;
         const int64_t hi = lo + per < v1 ? lo + per : v1;
         int64_t base = lo;
+        if (base + tile <= hi) {
+            Regs g;
+            load_batch(base + threadIdx.x, kBlock, g);
+            tables();
+            use_batch(base + threadIdx.x, kBlock, g);
+            base += tile;
+        } else {
+            tables();
+        }
         for (; base + tile <= hi; base += tile) batch(base + threadIdx.x, kBlock);
         for (int64_t u = base + threadIdx.x; u < hi; u += kBlock) one(u);
     } else {
+        tables();
         for (int64_t v = e0 / N + (int64_t)blockIdx.x * kBlock + threadIdx.x; v < v1; v += stride * U) {
             if (v + (U - 1) * stride < v1) {
                 batch(v, stride);

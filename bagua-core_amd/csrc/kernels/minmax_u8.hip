@@ -159,6 +159,25 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
     const int64_t len = e1 - e0;
     const S* src = in + (int64_t)c * cs + e0;
     uint8_t* seg = out + (int64_t)c * chunk_offset;
+    uint8_t* payload = seg + 32 + e0;
+    const int a = common_alignment<T>((uintptr_t)src, (uintptr_t)payload);
+    const int64_t j0 = a < 0 ? len : (a < len ? a : len);
+    const int64_t nvec = a < 0 ? 0 : (len - j0) / N;
+    const uint4* __restrict__ vsrc = reinterpret_cast<const uint4*>(src + j0);
+    uint8_t* vdst = payload + j0;
+    const int64_t ntiles = (nvec + kVecPerBlockTile - 1) / kVecPerBlockTile;
+    // the first tile's loads go out before the partials fold below (they do not need
+    // the chunk's parameters): a workgroup otherwise starts with an L2 round trip and a
+    // barrier and no HBM request in flight -- with ~4 workgroups per CU slot per launch
+    // that idle start recurred four times per slot
+    uint4 pre[kSubtiles];
+    const int64_t t_first = blockIdx.x;
+    const int64_t base_first = (kReverse ? (ntiles - 1 - t_first) : t_first) * kVecPerBlockTile;
+    const bool have_pre = t_first < ntiles && base_first + kVecPerBlockTile <= nvec;
+    if (have_pre) {
+#pragma unroll
+        for (int k = 0; k < kSubtiles; ++k) pre[k] = nt_load16(&vsrc[base_first + k * kBlock + threadIdx.x]);
+    }
 
     // fold the chunk's partials (written by pass 1; L2/MALL-resident)
     uint32_t lo = 0xffffffffu, hi = 0xffffffffu;
@@ -199,19 +218,21 @@ __global__ __launch_bounds__(kBlock) void minmax_quantize_kernel(
                 out[j] = 0;
     }
 
-    uint8_t* payload = seg + 32 + e0;
-    const int a = common_alignment<T>((uintptr_t)src, (uintptr_t)payload);
     if (a < 0) {  // no common vector alignment: scalar path over the whole chunk
         for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < len; j += (int64_t)gridDim.x * kBlock)
             payload[j] = (uint8_t)quant(T::to_f(src[j]), q);
         return;
     }
-    const int64_t j0 = a < len ? a : len;
-    const int64_t nvec = (len - j0) / N;
-    const uint4* __restrict__ vsrc = reinterpret_cast<const uint4*>(src + j0);
-    uint8_t* vdst = payload + j0;
-    const int64_t ntiles = (nvec + kVecPerBlockTile - 1) / kVecPerBlockTile;
-    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    if (have_pre) {
+#pragma unroll
+        for (int k = 0; k < kSubtiles; ++k) {
+            const int64_t v = base_first + k * kBlock + threadIdx.x;
+            float f[N];
+            unpack16<T>(pre[k], f);
+            quant_store_vec<T>(f, q, vdst + v * N);
+        }
+    }
+    for (int64_t t = blockIdx.x + (have_pre ? gridDim.x : 0); t < ntiles; t += gridDim.x) {
         const int64_t base = (kReverse ? (ntiles - 1 - t) : t) * kVecPerBlockTile;
         if (base + kVecPerBlockTile <= nvec) {
             // full tile: all loads issued before any is consumed
@@ -254,34 +275,50 @@ __global__ __launch_bounds__(kBlock) void minmax_dequantize_kernel(
     constexpr int N = Vec<T>::N;
     const int c = blockIdx.y;
     const uint8_t* seg = in + (int64_t)c * chunk_offset;
-    const QParams q = read_header<T>(seg);
     const uint8_t* payload = seg + 32 + e0;
     S* dst = out + (int64_t)c * cs + e0;
     const int64_t len = e1 - e0;
+    const int a = common_alignment<T>((uintptr_t)dst, (uintptr_t)payload);
+    const int64_t j0 = a < 0 ? len : (a < len ? a : len);
+    const int64_t nvec = a < 0 ? 0 : (len - j0) / N;
+    uint4* __restrict__ vdst = reinterpret_cast<uint4*>(dst + j0);
+    const uint8_t* vsrc = payload + j0;
+    const int64_t stride = (int64_t)gridDim.x * kVecPerBlockTile;
+    using W = typename Vec<T>::out_bytes;  // the N payload bytes of one vector
+    // the first tile's payload loads go out before the header read and the table build
+    // (one tile per workgroup up to 1 GiB: that prologue was the workgroup's whole
+    // latency, with no HBM request in flight)
+    W pre[kSubtiles];
+    const int64_t base_first = (int64_t)blockIdx.x * kVecPerBlockTile;
+    const bool have_pre = base_first + kVecPerBlockTile <= nvec;
+    if (have_pre) {
+#pragma unroll
+        for (int k = 0; k < kSubtiles; ++k) pre[k] = load_word<T>(vsrc + (base_first + k * kBlock + threadIdx.x) * N);
+    }
+    const QParams q = read_header<T>(seg);
     static_assert(kBlock == 256, "one table entry per thread");
     __shared__ uint32_t lut[256];  // stored T bits of every byte value (codec_common.hpp)
     lut[threadIdx.x] = stored_bits<T>(dequant(threadIdx.x, q));
     __syncthreads();
 
-    const int a = common_alignment<T>((uintptr_t)dst, (uintptr_t)payload);
     if (a < 0) {
         for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < len; j += (int64_t)gridDim.x * kBlock)
             dst[j] = storage_from_bits<T>(lut[payload[j]]);
         return;
     }
-    const int64_t j0 = a < len ? a : len;
-    const int64_t nvec = (len - j0) / N;
-    uint4* __restrict__ vdst = reinterpret_cast<uint4*>(dst + j0);
-    const uint8_t* vsrc = payload + j0;
-    const int64_t stride = (int64_t)gridDim.x * kVecPerBlockTile;
-    using W = typename Vec<T>::out_bytes;  // the N payload bytes of one vector
-    for (int64_t base = (int64_t)blockIdx.x * kVecPerBlockTile; base < nvec; base += stride) {
+    for (int64_t base = base_first; base < nvec; base += stride) {
         if (base + kVecPerBlockTile <= nvec) {
             // full tile: raw loads first (no unpacking inside the load block, or
             // each load gets its own vmcnt(0) wait), then dequantise and store
             W raw[kSubtiles];
+            if (base == base_first) {
 #pragma unroll
-            for (int k = 0; k < kSubtiles; ++k) raw[k] = load_word<T>(vsrc + (base + k * kBlock + threadIdx.x) * N);
+                for (int k = 0; k < kSubtiles; ++k) raw[k] = pre[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < kSubtiles; ++k)
+                    raw[k] = load_word<T>(vsrc + (base + k * kBlock + threadIdx.x) * N);
+            }
 #pragma unroll
             for (int k = 0; k < kSubtiles; ++k) {
                 uint32_t b[N];
@@ -349,6 +386,22 @@ __global__ __launch_bounds__(kBlock) void minmax_one_rank_kernel(typename T::sto
                                                                  const uint2* __restrict__ partials, int npartials) {
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
+    // the body on 16-B vectors (head elements before the first aligned one go scalar)
+    int64_t j0 = (int64_t)(((16u - ((uintptr_t)x & 15u)) & 15u) / sizeof(S));
+    if (((uintptr_t)x % sizeof(S)) != 0) j0 = n;
+    if (j0 > n) j0 = n;
+    const int64_t nvec = (n - j0) / N;
+    uint4* __restrict__ v = reinterpret_cast<uint4*>(x + j0);
+    const int64_t ntiles = (nvec + kVecPerBlockTile - 1) / kVecPerBlockTile;
+    // the first tile's loads go out before the partials fold and the table build (the
+    // workgroup's prologue otherwise runs with no HBM request in flight)
+    uint4 pre[kSubtiles];
+    const int64_t base_first = (ntiles - 1 - (int64_t)blockIdx.x) * kVecPerBlockTile;
+    const bool have_pre = (int64_t)blockIdx.x < ntiles && base_first + kVecPerBlockTile <= nvec;
+    if (have_pre) {
+#pragma unroll
+        for (int k = 0; k < kSubtiles; ++k) pre[k] = nt_load16(&v[base_first + k * kBlock + threadIdx.x]);
+    }
     uint32_t lo = 0xffffffffu, hi = 0xffffffffu;
     for (int i = threadIdx.x; i < npartials; i += kBlock) {
         const uint2 p = partials[i];
@@ -385,21 +438,19 @@ __global__ __launch_bounds__(kBlock) void minmax_one_rank_kernel(typename T::sto
     lut[threadIdx.x] = stored_bits<T>(dequant(quant(y_of(threadIdx.x), q2), q2));
     __syncthreads();
 
-    // the body on 16-B vectors (head elements before the first aligned one go scalar)
-    int64_t j0 = (int64_t)(((16u - ((uintptr_t)x & 15u)) & 15u) / sizeof(S));
-    if (((uintptr_t)x % sizeof(S)) != 0) j0 = n;
-    if (j0 > n) j0 = n;
-    const int64_t nvec = (n - j0) / N;
-    uint4* __restrict__ v = reinterpret_cast<uint4*>(x + j0);
-    const int64_t ntiles = (nvec + kVecPerBlockTile - 1) / kVecPerBlockTile;
     // reverse sweep: the min/max pass read the tail last, so it is re-read from the
     // Infinity Cache first
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int64_t base = (ntiles - 1 - t) * kVecPerBlockTile;
         if (base + kVecPerBlockTile <= nvec) {
             uint4 r[kSubtiles];
+            if (t == (int64_t)blockIdx.x) {
 #pragma unroll
-            for (int k = 0; k < kSubtiles; ++k) r[k] = nt_load16(&v[base + k * kBlock + threadIdx.x]);
+                for (int k = 0; k < kSubtiles; ++k) r[k] = pre[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < kSubtiles; ++k) r[k] = nt_load16(&v[base + k * kBlock + threadIdx.x]);
+            }
 #pragma unroll
             for (int k = 0; k < kSubtiles; ++k) {
                 float f[N];

@@ -196,6 +196,66 @@ __device__ __forceinline__ float tile_from(const float* v, int64_t base, int64_t
     return wave_tree_sum(lane_tree(a));
 }
 
+// The fixed 1024-tree over a chunk's m1 tile partials get(r), by one
+// kObFinalizeThreads workgroup: level 1 -> 2 straight from `get` (each wave takes
+// kFinBatch groups at once and issues all their loads -- clamped, unconditional --
+// before any tree, so the pass costs one memory latency instead of one per group),
+// the higher levels in LDS.  Every thread returns the total (0 when m1 = 0).
+template <typename Get>
+__device__ __forceinline__ float chunk_tree(const Get& get, int64_t m1, float (&lvl)[2][2048]) {
+    const int lane = lane_id(), wave = threadIdx.x / kWave, nw = kObFinalizeThreads / kWave;
+    if (m1 <= 0) return 0.0f;
+    int64_t m = m1;
+    const int64_t g1 = (m + kObTile - 1) / kObTile;
+    constexpr int kFinBatch = 4;
+    for (int64_t g0 = wave; g0 < g1; g0 += (int64_t)nw * kFinBatch) {
+        float a[kFinBatch][4][4];
+        if ((g0 + (int64_t)(kFinBatch - 1) * nw + 1) * kObTile <= m) {
+            // every group of the batch is full: one base per group, immediate offsets
+#pragma unroll
+            for (int j = 0; j < kFinBatch; ++j) {
+                const int64_t bj = (g0 + (int64_t)j * nw) * kObTile + lane * 4;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) a[j][k][e] = get(bj + k * 256 + e);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kFinBatch; ++j)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int64_t r = (g0 + (int64_t)j * nw) * kObTile + k * 256 + lane * 4 + e;
+                        a[j][k][e] = r < m ? get(r) : 0.0f;
+                    }
+        }
+#pragma unroll
+        for (int j = 0; j < kFinBatch; ++j) {
+            const int64_t g = g0 + (int64_t)j * nw;
+            const float s = wave_tree_sum(lane_tree(a[j]));
+            if (lane == 0 && g < g1) lvl[0][g] = s;
+        }
+    }
+    __syncthreads();
+    int cur = 0;
+    bool done = m <= kObTile;
+    m = g1;
+    while (!done) {
+        const int64_t g = (m + kObTile - 1) / kObTile;
+        for (int64_t i = wave; i < g; i += nw) {
+            const float s = tile_from(lvl[cur], i * kObTile, m, lane);
+            if (lane == 0) lvl[cur ^ 1][i] = s;
+        }
+        __syncthreads();
+        done = m <= kObTile;
+        cur ^= 1;
+        m = g;
+    }
+    return lvl[cur][0];
+}
+
 __global__ __launch_bounds__(kObFinalizeThreads) void onebit_finalize_kernel(
     const float* __restrict__ partials, int64_t tiles_per_chunk, int64_t in_num_elem, int64_t cs, int target,
     uint8_t* __restrict__ out, int64_t chunk_offset, int64_t out_bytes, int num_chunks) {
@@ -204,62 +264,7 @@ __global__ __launch_bounds__(kObFinalizeThreads) void onebit_finalize_kernel(
     const int64_t n = ob_valid(in_num_elem, cs, c);
     const float* part = partials + (int64_t)blockIdx.x * tiles_per_chunk;
     const int64_t m1 = (n + kObTile - 1) / kObTile;  // tiles holding valid elements
-    const int lane = lane_id(), wave = threadIdx.x / kWave, nw = kObFinalizeThreads / kWave;
-    float total = 0.0f;
-    if (m1 > 0) {
-        // level 1 -> 2 from global memory: each wave takes kFinBatch groups at
-        // once and issues all their loads (clamped, unconditional) before any
-        // tree, so the pass costs one memory latency instead of one per group
-        int64_t m = m1;
-        const int64_t g1 = (m + kObTile - 1) / kObTile;
-        constexpr int kFinBatch = 4;
-        for (int64_t g0 = wave; g0 < g1; g0 += (int64_t)nw * kFinBatch) {
-            float a[kFinBatch][4][4];
-            if ((g0 + (int64_t)(kFinBatch - 1) * nw + 1) * kObTile <= m) {
-                // every group of the batch is full: one base per group, immediate offsets
-#pragma unroll
-                for (int j = 0; j < kFinBatch; ++j) {
-                    const float* pj = part + (g0 + (int64_t)j * nw) * kObTile + lane * 4;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) a[j][k][e] = pj[k * 256 + e];
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < kFinBatch; ++j)
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const int64_t r = (g0 + (int64_t)j * nw) * kObTile + k * 256 + lane * 4 + e;
-                            a[j][k][e] = r < m ? part[r] : 0.0f;
-                        }
-            }
-#pragma unroll
-            for (int j = 0; j < kFinBatch; ++j) {
-                const int64_t g = g0 + (int64_t)j * nw;
-                const float s = wave_tree_sum(lane_tree(a[j]));
-                if (lane == 0 && g < g1) lvl[0][g] = s;
-            }
-        }
-        __syncthreads();
-        int cur = 0;
-        bool done = m <= kObTile;
-        m = g1;
-        while (!done) {
-            const int64_t g = (m + kObTile - 1) / kObTile;
-            for (int64_t i = wave; i < g; i += nw) {
-                const float s = tile_from(lvl[cur], i * kObTile, m, lane);
-                if (lane == 0) lvl[cur ^ 1][i] = s;
-            }
-            __syncthreads();
-            done = m <= kObTile;
-            cur ^= 1;
-            m = g;
-        }
-        total = lvl[cur][0];
-    }
+    const float total = chunk_tree([part](int64_t r) { return part[r]; }, m1, lvl);
     uint8_t* seg = out + (int64_t)c * chunk_offset;
     if (threadIdx.x < 32) {
         const float scale = n > 0 ? total / (float)n : 0.0f;
@@ -561,6 +566,94 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
 }
 
 // ------------------------------------------------------------------------
+// The centralized op at one rank (centralized_low_precision_synchronous.rs:30-71
+// with p = 1: encode -> alltoall of the own bytes -> decode + reduce + re-encode
+// -> allgather of nothing -> decode) in two streaming passes.  At p = 1 the fused
+// middle step's table (onebit_reduce_encode_lut_kernel) has two entries: every
+// reduced element is v0 (its sign bit 0) or v1 (bit 1), and |v0| == |v1| (the
+// rounding to T and the tree's additions of 0 are sign-symmetric), so
+//   re-encoded bit  = bit ? (v1 < 0) : (v0 < 0)
+//   re-encoded scale = F(|v0| at every valid position, 0 past n) / n
+// with F the encoder's fixed tree: every full tile has one partial, the ragged
+// last tile another, and chunk_tree folds them exactly as the finalize would
+// fold stored partials.  onebit_one_rank_kernel (one workgroup) derives scale1
+// from the encode's tile partials, then v0, v1 and scale2; the decode writes
+// bit2 ? -scale2 : +scale2 from the encode's bits.  The reduced chunk, the second
+// bit plane and the table kernel (VALU-bound, 0.11 of HBM peak at 1 GiB) are gone;
+// the bytes are the 1-bit op's (bit-identical to the multi-kernel sequence).
+// ------------------------------------------------------------------------
+struct OneRankOut {
+    float scale2;
+    uint32_t mpos, mneg;  // all-ones when v0 < 0 / v1 < 0 (re-encoded bit of a 0 / 1 bit)
+    uint32_t pad;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kObFinalizeThreads) void onebit_one_rank_kernel(const float* __restrict__ partials,
+                                                                            int64_t n, int average, float pf,
+                                                                            OneRankOut* __restrict__ out) {
+    __shared__ float lvl[2][2048];
+    const int64_t m1 = (n + kObTile - 1) / kObTile;
+    const float total1 = chunk_tree([partials](int64_t r) { return partials[r]; }, m1, lvl);
+    __syncthreads();  // every thread has read the first tree's root before lvl is reused
+    const float scale1 = n > 0 ? total1 / (float)n : 0.0f;
+    // the table kernel's p = 1 entries: segment 0 decodes to +-scale1 as stored in T
+    const float pos[1] = {as_stored<T>(scale1)}, neg[1] = {as_stored<T>(-scale1)};
+    const float t0 = lut_tree<2>(0, 1, pos, neg), t1 = lut_tree<2>(1, 1, pos, neg);
+    const float v0 = as_stored<T>(average ? t0 / pf : t0);
+    const float v1 = as_stored<T>(average ? t1 / pf : t1);
+    // the re-encode's tile partials: a full tile of |v|, and the ragged last tile
+    const int lane = lane_id();
+    const float a = __builtin_fabsf(v0);
+    float full[4][4], last[4][4];
+    const int64_t rem = n % kObTile;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            full[k][e] = a;
+            last[k][e] = (k * 256 + lane * 4 + e) < rem ? a : 0.0f;
+        }
+    const float pfull = wave_tree_sum(lane_tree(full));
+    const float plast = rem ? wave_tree_sum(lane_tree(last)) : pfull;
+    const int64_t nfull = n / kObTile;
+    const float total2 = chunk_tree([=](int64_t r) { return r < nfull ? pfull : plast; }, m1, lvl);
+    if (threadIdx.x == 0) {
+        OneRankOut o;
+        o.scale2 = n > 0 ? total2 / (float)n : 0.0f;
+        o.mpos = v0 < 0.0f ? 0xffffffffu : 0u;
+        o.mneg = v1 < 0.0f ? 0xffffffffu : 0u;
+        o.pad = 0;
+        *out = o;
+    }
+}
+
+template <typename T, bool NTS>
+__global__ __launch_bounds__(kBlock) void onebit_one_rank_decode_kernel(const uint8_t* __restrict__ bits,
+                                                                       const OneRankOut* __restrict__ o,
+                                                                       int64_t cs, typename T::storage* __restrict__ out,
+                                                                       int64_t tiles) {
+    using S = typename T::storage;
+    const bool vec = ((uintptr_t)out % (4 * sizeof(S))) == 0;
+    const int lane = lane_id();
+    const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    const uint32_t sbits = __float_as_uint(o->scale2), mpos = o->mpos, mneg = o->mneg;
+    for (int64_t t = wave; t < tiles; t += nwaves) {
+        const uint32_t f1 = reinterpret_cast<const uint16_t*>(bits + t * kObTileBytes)[lane];
+        const uint32_t field = (f1 & mneg) | (~f1 & mpos);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float f[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)  // bit ? -scale2 : +scale2, as a sign-bit flip
+                f[e] = __uint_as_float(sbits ^ ((field << (31 - (k * 4 + e))) & 0x80000000u));
+            store4<T, NTS>(out, t * kObTile + k * 256 + lane * 4, cs, vec, f);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
 // host
 // ------------------------------------------------------------------------
 static int64_t ob_tiles(int64_t cs) { return (cs + kObTile - 1) / kObTile; }
@@ -712,11 +805,64 @@ static int ob_reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int
     return check_launch();
 }
 
+// workspace of the one-rank op: [0, 32) OneRankOut, the encode's bit tiles at 32,
+// its tile partials after them (256-B aligned)
+static int64_t onerank_partials_offset(int64_t tiles) { return (32 + tiles * kObTileBytes + 255) / 256 * 256; }
+
+template <typename T>
+static int ob_one_rank_impl(void* tensor, int n, int average, void* ws, size_t ws_bytes, hipStream_t s) {
+    using S = typename T::storage;
+    if (n < 0 || (!tensor && n > 0) || !ws || (uintptr_t)ws % 16) return BAGUA_ERR_INVALID_ARG;
+    const int64_t tiles = ob_tiles(n);
+    const int64_t off = onerank_partials_offset(tiles);
+    if (ws_bytes < (size_t)(off + (tiles > 0 ? tiles : 1) * (int64_t)sizeof(float))) return BAGUA_ERR_WORKSPACE;
+    uint8_t* seg = static_cast<uint8_t*>(ws);
+    float* partials = reinterpret_cast<float*>(seg + off);
+    // 1. sign bits + |x| tile partials of the whole tensor (one chunk)
+    if (tiles > 0) {
+        const int rc = ob_compress_impl<T>(tensor, n, n, 1, seg, (size_t)(32 + tiles * kObTileBytes), partials,
+                                           (size_t)tiles * sizeof(float), -1, s, 1, 0, tiles);
+        if (rc) return rc;
+    }
+    // 2. scale1, the two reduced values, scale2
+    launch(onebit_one_rank_kernel<T>, dim3(1), dim3(kObFinalizeThreads), 0, s, partials, (int64_t)n, average, 1.0f,
+           reinterpret_cast<OneRankOut*>(seg));
+    // 3. the result, from the bits (store policy as the decode's, by size)
+    if (tiles > 0) {
+        const int env = tune_int("BAGUA_OB_DECODE_NT", -1);
+        const int nt = env >= 0 ? env : ((int64_t)n * (int64_t)sizeof(S) > ((int64_t)256 << 20) ? 1 : 0);
+        const dim3 grid(ob_blocks(tiles, 1, tune_int("BAGUA_TUNE_OB_DECODE_BLOCKS", kObDecodeBlocks)));
+        if (nt == 1)
+            launch(onebit_one_rank_decode_kernel<T, true>, grid, dim3(kBlock), 0, s, seg + 32,
+                   reinterpret_cast<const OneRankOut*>(seg), (int64_t)n, static_cast<S*>(tensor), tiles);
+        else
+            launch(onebit_one_rank_decode_kernel<T, false>, grid, dim3(kBlock), 0, s, seg + 32,
+                   reinterpret_cast<const OneRankOut*>(seg), (int64_t)n, static_cast<S*>(tensor), tiles);
+    }
+    return check_launch();
+}
+
 }  // namespace bagua
 
 using namespace bagua;
 
 extern "C" {
+
+size_t bagua_onebit_one_rank_workspace_bytes(int num_elem) {
+    const int64_t tiles = ob_tiles(num_elem < 0 ? 0 : num_elem);
+    return (size_t)(onerank_partials_offset(tiles) + (tiles > 0 ? tiles : 1) * (int64_t)sizeof(float));
+}
+
+int bagua_onebit_centralized_one_rank(int dtype, void* tensor, int num_elem, int average, void* workspace,
+                                      size_t workspace_bytes, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+        case BAGUA_DTYPE_F32: return ob_one_rank_impl<F32>(tensor, num_elem, average, workspace, workspace_bytes, s);
+        case BAGUA_DTYPE_F16: return ob_one_rank_impl<F16>(tensor, num_elem, average, workspace, workspace_bytes, s);
+        case BAGUA_DTYPE_BF16: return ob_one_rank_impl<BF16>(tensor, num_elem, average, workspace, workspace_bytes, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
 
 size_t bagua_onebit_compressed_bytes(int chunk_size, int num_chunks) {
     return (size_t)num_chunks * (32 + (size_t)ob_tiles(chunk_size) * kObTileBytes);

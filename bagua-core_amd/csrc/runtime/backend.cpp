@@ -14,8 +14,13 @@
 //     ops, datatypes/mod.rs:963-1070), runs the bucket's comm ops through the
 //     C ABI (comm_ops.cpp) and marks the item done (lib.rs:209-254);
 //   * wait_pending_comm_ops waits for every scheduled item (lib.rs:321-337);
-//   * a monitor logs an op that runs longer than 300 s (lib.rs:255-265; the
-//     reference panics the process, here the failure is logged and kept).
+//   * a monitor fails an op that runs longer than 300 s (lib.rs:255-265,
+//     BAGUA_COMM_OP_TIMEOUT_S or bagua_comm_backend_set_op_timeout_ms): the
+//     reference panics and its hook exits the process (py/lib.rs:498-504); here the
+//     monitor logs the op, keeps the message (bagua_comm_backend_failure_message),
+//     aborts the op's communicators -- ncclCommAbort releases RCCL kernels waiting
+//     for a peer that never comes, the loopback transport breaks its barrier -- and
+//     wait_pending_comm_ops returns BAGUA_ERR_ABORTED instead of waiting forever.
 //   * cross-bucket pipelining (async mode, BAGUA_SCHED_LANES, default 3): bucket
 //     i of the registration order runs its ops on lane 1 + i % lanes of its
 //     communicator -- a view with its own streams (comm_internal.hpp) -- so the
@@ -30,6 +35,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 
 #include <chrono>
 #include <cstdio>
@@ -302,6 +308,10 @@ struct Scheduled {
     std::vector<bagua_bucket_op_t> ops;    // the bucket's ops at scheduling time
     bool done = false;                     // executed (sync) / enqueued (async)
     int status = BAGUA_OK;
+    std::chrono::steady_clock::time_point started;  // the worker picked it up (monitor clock)
+    std::atomic<bool> timed_out{false};    // the monitor aborted its communicators
+    std::atomic<int64_t> abort_ns{0};      // when (steady clock)
+    bool waited = false;                   // wait_pending_comm_ops is done with it (guarded by mu)
     // async: an event recorded on the bucket's stream behind its work, shared by every
     // bucket the worker enqueued on that stream since the previous record (back to the
     // backend's pool with the last of them)
@@ -322,6 +332,10 @@ struct BaguaCommBackendC {
     std::shared_ptr<Scheduled> current;
     std::chrono::steady_clock::time_point current_start;
     std::vector<std::string> failures;
+    // items the worker picked up and the monitor watches until their work completed
+    std::deque<std::shared_ptr<Scheduled>> inflight;
+    std::vector<std::shared_ptr<Scheduled>> stuck;  // abandoned items (their worker call never returned)
+    std::chrono::milliseconds op_timeout{300000};  // lib.rs:255-265 (BAGUA_COMM_OP_TIMEOUT_S)
     bool stop = false;
     bool async = true;                  // BAGUA_BACKEND_SYNC=1: every op waits for its stream
     // BAGUA_SCHED_LANES (async only; 1 = every bucket on the comm's stream).  3: 32 x 25 MiB at
@@ -438,6 +452,9 @@ struct BaguaCommBackendC {
                 cv_space.notify_all();
                 current = item;
                 current_start = std::chrono::steady_clock::now();
+                item->started = current_start;
+                while (!inflight.empty() && inflight.front()->waited) inflight.pop_front();
+                inflight.push_back(item);
             }
             const clk::time_point t_exec = clk::now();
             int nl;
@@ -453,7 +470,7 @@ struct BaguaCommBackendC {
             bool idle = false;
             {
                 std::lock_guard<std::mutex> lk(mu);
-                item->status = rc;
+                if (item->status == BAGUA_OK) item->status = rc;  // the monitor's ABORTED stays
                 if (!async) item->done = true;
                 current.reset();
                 idle = channel.empty();
@@ -471,19 +488,99 @@ struct BaguaCommBackendC {
         }
     }
 
+    // A watched item's work is over: executed (sync) or its completion event reached
+    // (async; a bucket without one failed or was waited for already).  Caller holds mu.
+    static bool settled_locked(const Scheduled& it, std::shared_ptr<void>* ev) {
+        if (!it.done) return false;
+        *ev = it.finished;
+        return !it.finished;
+    }
+
+    std::condition_variable cv_watch;
+
     void watch() {
         std::unique_lock<std::mutex> lk(mu);
         while (!stop) {
-            cv_work.wait_for(lk, std::chrono::seconds(5));
-            if (current && std::chrono::steady_clock::now() - current_start > std::chrono::seconds(300)) {
-                const std::string msg = "comm op on bucket " + current->bucket->name + " has not finished for 5 min";
-                bool seen = false;
-                for (const std::string& f : failures) seen = seen || f == msg;
-                if (!seen) {
-                    failures.push_back(msg);
-                    BAGUA_LOG(0, "%s", msg.c_str());
+            // tick: a quarter of the limit, between 10 ms and 5 s
+            const auto tick = std::max(std::chrono::milliseconds(10),
+                                       std::min(std::chrono::milliseconds(5000), op_timeout / 4));
+            cv_watch.wait_for(lk, tick);
+            if (stop) break;
+            const auto now = std::chrono::steady_clock::now();
+            std::vector<std::shared_ptr<Scheduled>> expired;
+            for (auto it = inflight.begin(); it != inflight.end();) {
+                std::shared_ptr<void> ev;
+                bool over = (*it)->waited || settled_locked(**it, &ev);
+                if (!over && ev) {
+                    const hipError_t q = hipEventQuery((hipEvent_t)ev.get());
+                    over = q != hipErrorNotReady;
+                    if (q != hipSuccess && q != hipErrorNotReady) (void)hipGetLastError();
                 }
+                if ((*it)->waited || over || (*it)->timed_out.load()) {
+                    it = inflight.erase(it);
+                    continue;
+                }
+                if (now - (*it)->started > op_timeout) {
+                    expired.push_back(*it);
+                    it = inflight.erase(it);
+                    continue;
+                }
+                ++it;
             }
+            if (expired.empty()) continue;
+            for (const auto& item : expired) {
+                const long long s_lim = (long long)(op_timeout.count() / 1000);
+                const std::string msg = "comm op on bucket " + item->bucket->name + " has not finished for " +
+                                        (s_lim ? std::to_string(s_lim) + " s"
+                                               : std::to_string((long long)op_timeout.count()) + " ms") +
+                                        "; its communicators are aborted";
+                failures.push_back(msg);
+                BAGUA_LOG(0, "%s", msg.c_str());
+                if (item->status == BAGUA_OK) item->status = BAGUA_ERR_ABORTED;
+            }
+            lk.unlock();  // an abort may wait for calls inside RCCL
+            for (const auto& item : expired) {
+                for (const bagua_bucket_op_t& op : item->ops) {
+                    if (op.comm) (void)bagua_comm_abort(op.comm);
+                    if (op.intranode) (void)bagua_comm_abort(op.intranode);
+                }
+                item->abort_ns.store(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                         std::chrono::steady_clock::now().time_since_epoch())
+                                         .count());
+                item->timed_out.store(true);
+            }
+            lk.lock();
+            cv_done.notify_all();
+        }
+    }
+
+    // How long wait_pending_comm_ops still waits for an aborted op's work to drain
+    // (RCCL kernels leave once their communicator is aborted; a transport that does not
+    // release them must not turn the failure into a hang)
+    static bool abandoned(const Scheduled& it) {
+        if (!it.timed_out.load()) return false;
+        const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                std::chrono::steady_clock::now().time_since_epoch())
+                                .count();
+        return now - it.abort_ns.load() > 10'000'000'000LL;
+    }
+
+    // the event completed (true), failed, or belongs to an abandoned op (false); polls,
+    // so the monitor's abort can end the wait
+    static bool wait_event(hipEvent_t e, const Scheduled& it) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t q = hipEventQuery(e);
+            if (q == hipSuccess) return true;
+            if (q != hipErrorNotReady) {
+                (void)hipGetLastError();
+                return false;
+            }
+            if (abandoned(it)) return false;
+            if (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(20))
+                std::this_thread::yield();
+            else
+                std::this_thread::sleep_for(std::chrono::microseconds(100));
         }
     }
 };
@@ -604,6 +701,8 @@ BaguaCommBackendC* bagua_comm_backend_create(size_t schedule_channel_cap, int de
     be->cap = schedule_channel_cap ? schedule_channel_cap : 1;
     const char* ln = std::getenv("BAGUA_SCHED_LANES");
     if (ln && *ln) be->lanes = std::max(1, std::min(8, std::atoi(ln)));
+    const char* to = std::getenv("BAGUA_COMM_OP_TIMEOUT_S");
+    if (to && *to && std::atof(to) > 0) be->op_timeout = std::chrono::milliseconds((long long)(std::atof(to) * 1000));
     const char* prof = std::getenv("BAGUA_SCHED_PROFILE");
     be->profile = prof && *prof && std::atoi(prof) != 0;
     be->worker = std::thread([be] { be->work(); });
@@ -619,6 +718,7 @@ void bagua_comm_backend_destroy(BaguaCommBackendC* be) {
     }
     be->cv_work.notify_all();
     be->cv_space.notify_all();
+    be->cv_watch.notify_all();
     // the worker drains what is queued, then exits; enqueued work is waited for
     if (be->worker.joinable()) be->worker.join();
     if (be->monitor.joinable()) be->monitor.join();
@@ -645,23 +745,29 @@ int bagua_comm_backend_wait_pending_comm_ops(BaguaCommBackendC* be, int* complet
     while (!be->pending.empty()) {
         std::vector<std::shared_ptr<Scheduled>> items(be->pending.begin(), be->pending.end());
         be->pending.clear();
-        for (const auto& item : items) be->cv_done.wait(lk, [&] { return item->done; });
+        for (const auto& item : items)
+            while (!item->done && !be->abandoned(*item)) be->cv_done.wait_for(lk, std::chrono::milliseconds(100));
         lk.unlock();
-        // one synchronisation per distinct completion event (buckets share them)
+        // one wait per distinct completion event (buckets share them)
         std::vector<std::pair<void*, bool>> synced;
         for (const auto& item : items) {
             void* e = item->finished.get();
             if (!e) continue;
             bool seen = false;
             for (const auto& x : synced) seen = seen || x.first == e;
-            if (!seen) synced.emplace_back(e, hipEventSynchronize((hipEvent_t)e) == hipSuccess);
+            if (!seen) synced.emplace_back(e, be->wait_event((hipEvent_t)e, *item));
         }
         lk.lock();
         for (const auto& item : items) {
+            if (!item->done) {  // abandoned: its worker never returned from the aborted op
+                if (item->status == BAGUA_OK) item->status = BAGUA_ERR_ABORTED;
+                be->stuck.push_back(item);  // kept, never reused
+            }
             for (const auto& x : synced)
                 if (x.first == item->finished.get() && !x.second && item->status == BAGUA_OK)
-                    item->status = BAGUA_ERR_HIP;
+                    item->status = item->timed_out.load() ? BAGUA_ERR_ABORTED : BAGUA_ERR_HIP;
             item->finished.reset();
+            item->waited = true;
             ++n;
             if (rc == BAGUA_OK && item->status != BAGUA_OK) rc = item->status;
         }
@@ -752,6 +858,29 @@ int bagua_comm_backend_failures(BaguaCommBackendC* be) {
     if (!be) return -1;
     std::lock_guard<std::mutex> lk(be->mu);
     return (int)be->failures.size();
+}
+
+int bagua_comm_backend_failure_message(BaguaCommBackendC* be, int i, char* buf, size_t len) {
+    if (!be || i < 0) return -1;
+    std::lock_guard<std::mutex> lk(be->mu);
+    if ((size_t)i >= be->failures.size()) return -1;
+    const std::string& m = be->failures[(size_t)i];
+    if (buf && len) {
+        const size_t n = std::min(len - 1, m.size());
+        std::memcpy(buf, m.data(), n);
+        buf[n] = 0;
+    }
+    return (int)m.size();
+}
+
+int bagua_comm_backend_set_op_timeout_ms(BaguaCommBackendC* be, int64_t ms) {
+    if (!be || ms <= 0) return BAGUA_ERR_INVALID_ARG;
+    {
+        std::lock_guard<std::mutex> lk(be->mu);
+        be->op_timeout = std::chrono::milliseconds(ms);
+    }
+    be->cv_watch.notify_all();
+    return BAGUA_OK;
 }
 
 }  // extern "C"

@@ -42,6 +42,26 @@ Transport* make_rccl_transport(ncclComm_t comm);
 ncclDataType_t nccl_dtype(int d);
 int nccl_status(ncclResult_t r);
 
+// The environment switches that change WHICH collectives an op posts (its piece
+// schedule, its exchange pattern, the descriptor check).  Ranks that disagreed on
+// them would post different collectives: a crash on the loopback transport, a hang
+// over RCCL.  So they are read once, when a communicator is created, and over RCCL
+// every rank adopts rank 0's values (agree_schedule_config, communicator.cpp); an op
+// never reads them from its own rank's environment.
+struct ScheduleConfig {
+    int32_t pieces_cap = 4;        // BAGUA_PIPELINE_PIECES: most pieces per chunk (1 disables)
+    int32_t min_piece = 1 << 20;   // BAGUA_PIPELINE_MIN_PIECE: payload bytes per chunk piece
+    int32_t taper = 0;             // BAGUA_PIPELINE_TAPER=1: first/last piece half size
+    int32_t multipath = 0;         // BAGUA_RING_MULTIPATH=1: relayed ring exchange from 6 ranks
+    int32_t check = 0;             // BAGUA_CHECK_SCHEDULE=1: ranks compare op descriptors first
+    int32_t reserved[3] = {0, 0, 0};
+    bool operator==(const ScheduleConfig& o) const {
+        return pieces_cap == o.pieces_cap && min_piece == o.min_piece && taper == o.taper &&
+               multipath == o.multipath && check == o.check;
+    }
+};
+ScheduleConfig read_schedule_config();
+
 // set by the native scheduler's worker thread: comm ops it runs are async
 extern thread_local bool g_async_ops;
 
@@ -54,6 +74,8 @@ struct BaguaSingleCommunicatorC {
     int device_id = 0;
     hipStream_t stream = nullptr;
     std::atomic<bool> aborted{false};
+    bagua::ScheduleConfig cfg;  // fixed at creation, equal on every rank (see ScheduleConfig)
+    std::atomic<uint64_t> op_seq{0};  // ops checked so far (BAGUA_CHECK_SCHEDULE; a lane view counts on its parent)
     // pipelined ops: a second stream for the exchange of piece k while `stream`
     // runs the codec on piece k+1, and the events that order the two (lazy)
     hipStream_t side = nullptr;
@@ -65,10 +87,15 @@ struct BaguaSingleCommunicatorC {
     // Lane views (the scheduler's cross-bucket pipelining, backend.cpp): communicators
     // that share this one's transport, rank and device but own their streams, side
     // streams and events, so consecutive buckets' ops run on different streams and
-    // bucket b+1's codec prefix overlaps bucket b's exchange and tail.  RCCL runs the
-    // collectives of one communicator in issue order whatever the stream they are
-    // issued on, and the scheduler's one worker thread issues every lane's ops, so the
-    // collective order stays identical on every rank.  A view never owns the transport.
+    // bucket b+1's codec prefix overlaps bucket b's exchange and tail.  The claim this
+    // rests on: RCCL (the NCCL 2.27.7 code base of ROCm 7.2's librccl) runs one
+    // communicator's operations in the order they are issued whatever the user stream
+    // -- every launch of a communicator is chained behind the previous one on the
+    // communicator's internal device stream before the user stream joins it -- and the
+    // scheduler's one worker thread issues every lane's ops, so the collective order
+    // stays identical on every rank.  Pinned by test_native_scheduler_lanes_over_rccl
+    // (7 buckets x 2 steps on 3 lanes of one RCCL communicator, bit-exact against the
+    // oracle).  A view never owns the transport.
     BaguaSingleCommunicatorC* parent = nullptr;
     bool own_stream = false;
     std::mutex lanes_mu;
@@ -111,6 +138,10 @@ struct BaguaSingleCommunicatorC {
             (void)bagua_release_stream_resources(device_id, (uint64_t)(uintptr_t)stream);
             if (side) (void)bagua_release_stream_resources(device_id, (uint64_t)(uintptr_t)side);
         }
+        // a lane view's stream leaves the one-launch encode's opt-out set even when the
+        // stream itself is kept (aborted): a later stream reusing the handle value must
+        // not inherit the opt-out
+        if (own_stream && stream) (void)bagua_minmax_u8_set_stream_resident(stream, 1);
         for (hipEvent_t e : events) (void)hipEventDestroy(e);
         if (join) (void)hipEventDestroy(join);
         if (side) (void)hipStreamDestroy(side);

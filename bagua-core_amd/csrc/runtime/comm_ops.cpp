@@ -149,6 +149,10 @@ class OpBuffer {
     } while (0)
 
 int env_int(const char* name, long dflt);
+int check_schedule(BaguaSingleCommunicatorC* c, int op, int method, const bagua_tensor_t* t, uint64_t chunk,
+                   int sched, int average);
+enum { kOpCentralized = 1, kOpCentralizedUnfused, kOpCentralizedPipelined, kOpOneBitPipelined, kOpRing,
+       kOpRingUnfused, kOpRingPipelined };
 
 int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int average, int method, bool fused) {
     OpTimer tm;
@@ -167,6 +171,8 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
     int rc = plan(c, t, method, &k);
     if (rc) return rc;
     DeviceGuard guard(c->device_id);
+    if ((rc = check_schedule(c, fused ? kOpCentralized : kOpCentralizedUnfused, method, t, k.cs, 1, average)))
+        return rc;
     const uint64_t s = (uint64_t)(uintptr_t)c->stream;
     if (k.p == 1 && fused && method == BAGUA_COMPRESSION_MINMAX_UINT8 && t->num_elem == t->num_elem_allocated &&
         k.cs <= 0x7fffffffULL && env_int("BAGUA_ONE_RANK_FUSED", 1) != 0) {
@@ -179,6 +185,19 @@ int centralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int averag
         ph[0] = tm.lap();
         rc = bagua_minmax_u8_centralized_one_rank(t->dtype, (void*)(uintptr_t)t->ptr, (int)k.cs, average,
                                                   (void*)(uintptr_t)ws, ws_bytes, (void*)(uintptr_t)s);
+        ph[2] = tm.lap();
+        return finish(c, rc);
+    }
+    if (k.p == 1 && fused && method == BAGUA_COMPRESSION_ONEBIT && t->num_elem == t->num_elem_allocated &&
+        k.cs <= 0x7fffffffULL && env_int("BAGUA_ONE_RANK_FUSED", 1) != 0) {
+        // the same for the 1-bit codec: encode pass, one workgroup for both scales, one
+        // pass writing +-scale2 from the bits (bagua_onebit_centralized_one_rank)
+        const size_t ws_bytes = bagua_onebit_one_rank_workspace_bytes((int)k.cs);
+        uint64_t ws = 0;
+        if ((rc = stream_workspace(c->device_id, s, ws_bytes, &ws)) != BAGUA_OK) return finish(c, rc);
+        ph[0] = tm.lap();
+        rc = bagua_onebit_centralized_one_rank(t->dtype, (void*)(uintptr_t)t->ptr, (int)k.cs, average,
+                                               (void*)(uintptr_t)ws, ws_bytes, (void*)(uintptr_t)s);
         ph[2] = tm.lap();
         return finish(c, rc);
     }
@@ -281,26 +300,69 @@ int env_int(const char* name, long dflt) {
     return v && *v ? (int)std::strtol(v, nullptr, 10) : (int)dflt;
 }
 
-int auto_pieces(size_t payload_bytes) {
+int auto_pieces(const BaguaSingleCommunicatorC* c, size_t payload_bytes) {
     // BAGUA_PIPELINE_PIECES caps the count (1 disables), pieces keep at least
     // BAGUA_PIPELINE_MIN_PIECE payload bytes per chunk (= elements for MinMax
-    // u8; the exchange of a piece is p times that)
-    const int kmax = env_int("BAGUA_PIPELINE_PIECES", 4);
-    const int min_piece = env_int("BAGUA_PIPELINE_MIN_PIECE", 1 << 20);
+    // u8; the exchange of a piece is p times that); both read once, at the
+    // communicator's creation (ScheduleConfig)
+    const int kmax = c->cfg.pieces_cap;
+    const int min_piece = c->cfg.min_piece;
     size_t k = payload_bytes / (size_t)(min_piece > 0 ? min_piece : 1);
     if (k > (size_t)kmax) k = (size_t)kmax;
     return k < 1 ? 1 : (int)k;
 }
 
 // The op's piece schedule (bagua_kernels.h: a count, optionally OR-ed with
-// BAGUA_PIECES_TAPERED): the caller's, with BAGUA_PIPELINE_TAPER=1 tapering a
-// count >= 3 the caller left plain.  Read once per op, on the calling thread, and
-// passed to every building block, so all of one op's ranges agree.
-int op_schedule(int count, int caller) {
+// BAGUA_PIECES_TAPERED): the caller's, with BAGUA_PIPELINE_TAPER=1 (the
+// communicator's ScheduleConfig, equal on every rank) tapering a count >= 3 the
+// caller left plain.  Fixed once per op and passed to every building block, so all
+// of one op's ranges agree.
+int op_schedule(const BaguaSingleCommunicatorC* c, int count, int caller) {
     int sched = count | (caller & BAGUA_PIECES_TAPERED);
-    if (count >= 3 && !(sched & BAGUA_PIECES_TAPERED) && env_int("BAGUA_PIPELINE_TAPER", 0) == 1)
-        sched |= BAGUA_PIECES_TAPERED;
+    if (count >= 3 && !(sched & BAGUA_PIECES_TAPERED) && c->cfg.taper) sched |= BAGUA_PIECES_TAPERED;
     return sched;
+}
+
+// ---- BAGUA_CHECK_SCHEDULE: ranks compare what they are about to post ---------
+// Opt-in (ScheduleConfig::check, equal on every rank): before an op's first
+// collective the ranks allgather a small descriptor of the op -- which op, codec,
+// dtype, p, chunk size, tensor sizes, piece schedule, average, op number -- on the
+// op's own communicator and stream, and every rank returns BAGUA_ERR_INVALID_ARG
+// when any two differ, before any of them posts a collective the others do not
+// match (which over RCCL hangs; centralized_low_precision_synchronous.rs:30-71 is
+// the sequence every rank must post alike).  Costs one small allgather and a host
+// round trip per op.
+constexpr int kDescFields = 10;
+const char* const kDescName[kDescFields] = {"op",       "method",         "dtype",   "nranks",  "chunk elements",
+                                            "num_elem", "num_elem_alloc", "schedule", "average", "op number"};
+
+int check_schedule(BaguaSingleCommunicatorC* c, int op, int method, const bagua_tensor_t* t, uint64_t chunk,
+                   int sched, int average) {
+    if (!c->cfg.check || c->nranks <= 1) return BAGUA_OK;
+    BaguaSingleCommunicatorC* root = c->parent ? c->parent : c;
+    const int64_t mine[kDescFields] = {op, method, t->dtype, (int64_t)c->nranks, (int64_t)chunk, (int64_t)t->num_elem,
+                                       (int64_t)t->num_elem_allocated, sched, average != 0,
+                                       (int64_t)root->op_seq.fetch_add(1)};
+    const size_t one = sizeof(mine), p = c->nranks;
+    PoolBuffer buf;
+    int rc = buf.allocate(c->device_id, one * p);
+    if (rc) return rc;
+    std::vector<int64_t> all(kDescFields * p);
+    uint8_t* base = buf.as<uint8_t>();
+    if (hipMemcpyAsync(base + c->rank * one, mine, one, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return BAGUA_ERR_HIP;
+    if ((rc = c->t->allgather(base + c->rank * one, base, one, BAGUA_DTYPE_U8, c->stream)) != BAGUA_OK) return rc;
+    if (hipMemcpyAsync(all.data(), base, one * p, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return BAGUA_ERR_HIP;
+    for (size_t j = 0; j < p; ++j)
+        for (int f = 0; f < kDescFields; ++f)
+            if (all[j * kDescFields + f] != mine[f]) {
+                BAGUA_LOG(0, "rank %zu: op schedule mismatch with rank %zu: %s %lld here, %lld there", c->rank, j,
+                          kDescName[f], (long long)mine[f], (long long)all[j * kDescFields + f]);
+                return BAGUA_ERR_INVALID_ARG;
+            }
+    return BAGUA_OK;
 }
 
 bool valid_schedule(int pieces) {
@@ -435,14 +497,16 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
     if (rc) return rc;
     const int caller = pieces;
     pieces &= BAGUA_PIECES_COUNT_MASK;
-    if (pieces < 1) pieces = k.p == 1 ? 1 : auto_pieces(k.cs);  // one rank: no exchange to hide
+    if (pieces < 1) pieces = k.p == 1 ? 1 : auto_pieces(c, k.cs);  // one rank: no exchange to hide
     if (pieces == 1 || !pipeline_fits(c, t, k)) return centralized(c, t, average, BAGUA_COMPRESSION_MINMAX_UINT8, true);
     if (t->ptr % 16)
         return with_aligned_copy(c, {t}, [&](const std::vector<const bagua_tensor_t*>& u) {
             return centralized_pipelined(c, u[0], average, pieces | (caller & BAGUA_PIECES_TAPERED));
         });
-    const int sched = op_schedule(pieces, caller);
+    const int sched = op_schedule(c, pieces, caller);
     DeviceGuard guard(c->device_id);
+    if ((rc = check_schedule(c, kOpCentralizedPipelined, BAGUA_COMPRESSION_MINMAX_UINT8, t, k.cs, sched, average)))
+        return rc;
     if (c->ensure_side(4 * (size_t)pieces + 1)) return BAGUA_ERR_HIP;
     hipStream_t s0 = c->stream, s1 = c->side;
     hipEvent_t* quantised = c->events.data();
@@ -528,10 +592,11 @@ int centralized_pipelined_onebit(BaguaSingleCommunicatorC* c, const bagua_tensor
     int rc = plan(c, t, BAGUA_COMPRESSION_ONEBIT, &k);
     if (rc) return rc;
     pieces &= BAGUA_PIECES_COUNT_MASK;  // 1-bit pieces are tile ranges: no tapered schedule
-    if (pieces < 1) pieces = k.p == 1 ? 1 : auto_pieces(k.cs / 8);  // sign bits per chunk
+    if (pieces < 1) pieces = k.p == 1 ? 1 : auto_pieces(c, k.cs / 8);  // sign bits per chunk
     if (pieces == 1 || k.p > 16 || t->num_elem != t->num_elem_allocated || k.cs > 0x7fffffffULL)
         return centralized(c, t, average, BAGUA_COMPRESSION_ONEBIT, true);
     DeviceGuard guard(c->device_id);
+    if ((rc = check_schedule(c, kOpOneBitPipelined, BAGUA_COMPRESSION_ONEBIT, t, k.cs, pieces, average))) return rc;
     if (c->ensure_side(2 * (size_t)pieces + 2)) return BAGUA_ERR_HIP;
     hipStream_t s0 = c->stream, s1 = c->side;
     hipEvent_t* encoded = c->events.data();
@@ -753,12 +818,14 @@ int ring_exchange_group(BaguaSingleCommunicatorC* c, const RingPlan& P, int g, u
 }
 
 // Opt-in (BAGUA_PIECES_MULTIPATH in the op's `pieces`, or BAGUA_RING_MULTIPATH=1 read
-// once per op): the only timing so far is RCCL's socket
+// once at the communicator's creation): the only timing so far is RCCL's socket
 // transport between processes on one GPU, where multipath was 5.3x slower than
 // the direct exchange (profiles/r02_b_ar8_shared_gpu_rccl_socket.json); until an
 // xGMI node shows it faster, the default is the reference's direct exchange
 // (decentralized_low_precision_synchronous.rs:98-115).
-bool ring_multipath_enabled(int p) { return p >= kRingMinMultipath && env_int("BAGUA_RING_MULTIPATH", 0) != 0; }
+bool ring_multipath_enabled(const BaguaSingleCommunicatorC* c) {
+    return (int)c->nranks >= kRingMinMultipath && c->cfg.multipath;
+}
 
 }  // namespace
 
@@ -813,6 +880,17 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
         return with_aligned_copy(c, {t, weight, left, right}, [&](const std::vector<const bagua_tensor_t*>& u) {
             return decentralized(c, u[0], u[1], u[2], u[3], method, allow_fused, pieces);
         });
+    // the exchange schedule, from values equal on every rank (ScheduleConfig included)
+    const int caller = pieces;
+    pieces &= BAGUA_PIECES_COUNT_MASK;
+    if (pieces < 1) pieces = c->nranks == 1 ? 1 : auto_pieces(c, (size_t)n);
+    const int sched = op_schedule(c, pieces, caller);
+    const bool multipath =
+        (caller & BAGUA_PIECES_MULTIPATH) ? (int)c->nranks >= kRingMinMultipath : ring_multipath_enabled(c);
+    const bool pipelined = fused && (pieces > 1 || multipath);
+    if ((rc = check_schedule(c, pipelined ? kOpRingPipelined : (allow_fused ? kOpRing : kOpRingUnfused), method, t,
+                             (uint64_t)n, pipelined ? sched | (multipath ? BAGUA_PIECES_MULTIPATH : 0) : 1, 1)))
+        return rc;
     OpBuffer mine(c), lbuf(c), rbuf(c);
     TRY(mine.allocate(c->device_id, S));
     TRY(lbuf.allocate(c->device_id, S));
@@ -833,13 +911,7 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
         void* ws = (void*)(uintptr_t)wsp;
         rc = bagua_ring_mix_minmax(t->dtype, tp, lp, rp, wp, n, ws, wsb, sp);
         if (rc == BAGUA_OK) {
-            const int caller = pieces;
-            pieces &= BAGUA_PIECES_COUNT_MASK;
-            if (pieces < 1) pieces = c->nranks == 1 ? 1 : auto_pieces((size_t)n);
-            const int sched = op_schedule(pieces, caller);
-            const bool multipath = (caller & BAGUA_PIECES_MULTIPATH) ? (int)c->nranks >= kRingMinMultipath
-                                                                     : ring_multipath_enabled((int)c->nranks);
-            if (pieces > 1 || multipath) {
+            if (pipelined) {
                 // pipelined: quantise piece q -> exchange piece q (side stream) -> apply piece q;
                 // one header for the whole bucket, travelling with piece 0.  Multipath: the
                 // relayed slices of piece q arrive with group q + 1.

@@ -10,7 +10,11 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -86,43 +90,108 @@ class RcclTransport final : public Transport {
    public:
     explicit RcclTransport(ncclComm_t c) : comm_(c) {}
     ~RcclTransport() override {
-        if (comm_) (void)ncclCommDestroy(comm_);
+        if (comm_ && !aborted_.load()) (void)ncclCommDestroy(comm_);
     }
     int allreduce(const void* s, void* r, size_t n, int d, int op, hipStream_t st) override {
-        return nccl_status(ncclAllReduce(s, r, n, nccl_dtype(d), nccl_op(op), comm_, st));
+        Call g(this);
+        return g.ok ? nccl_status(ncclAllReduce(s, r, n, nccl_dtype(d), nccl_op(op), comm_, st)) : BAGUA_ERR_ABORTED;
     }
     int broadcast(void* b, size_t n, int d, int root, hipStream_t st) override {
-        return nccl_status(ncclBroadcast(b, b, n, nccl_dtype(d), root, comm_, st));
+        Call g(this);
+        return g.ok ? nccl_status(ncclBroadcast(b, b, n, nccl_dtype(d), root, comm_, st)) : BAGUA_ERR_ABORTED;
     }
     int reduce(const void* s, void* r, size_t n, int d, int op, int root, hipStream_t st) override {
-        return nccl_status(ncclReduce(s, r, n, nccl_dtype(d), nccl_op(op), root, comm_, st));
+        Call g(this);
+        return g.ok ? nccl_status(ncclReduce(s, r, n, nccl_dtype(d), nccl_op(op), root, comm_, st))
+                    : BAGUA_ERR_ABORTED;
     }
     int alltoall(const void* s, void* r, size_t n, int d, hipStream_t st) override {
-        return nccl_status(ncclAllToAll(s, r, n, nccl_dtype(d), comm_, st));
+        Call g(this);
+        return g.ok ? nccl_status(ncclAllToAll(s, r, n, nccl_dtype(d), comm_, st)) : BAGUA_ERR_ABORTED;
     }
     int allgather(const void* s, void* r, size_t n, int d, hipStream_t st) override {
-        return nccl_status(ncclAllGather(s, r, n, nccl_dtype(d), comm_, st));
+        Call g(this);
+        return g.ok ? nccl_status(ncclAllGather(s, r, n, nccl_dtype(d), comm_, st)) : BAGUA_ERR_ABORTED;
     }
     int send(const void* b, size_t n, int d, int peer, hipStream_t st) override {
-        return nccl_status(ncclSend(b, n, nccl_dtype(d), peer, comm_, st));
+        Call g(this);
+        return g.ok ? nccl_status(ncclSend(b, n, nccl_dtype(d), peer, comm_, st)) : BAGUA_ERR_ABORTED;
     }
     int recv(void* b, size_t n, int d, int peer, hipStream_t st) override {
-        return nccl_status(ncclRecv(b, n, nccl_dtype(d), peer, comm_, st));
+        Call g(this);
+        return g.ok ? nccl_status(ncclRecv(b, n, nccl_dtype(d), peer, comm_, st)) : BAGUA_ERR_ABORTED;
     }
+    // group brackets stay balanced after an abort (the calls between them fail)
     int group_start() override { return nccl_status(ncclGroupStart()); }
     int group_end() override { return nccl_status(ncclGroupEnd()); }
+    // From any thread (the scheduler's monitor aborts a stuck op's communicator while
+    // the worker may be enqueueing): later calls fail with BAGUA_ERR_ABORTED; calls
+    // already inside RCCL get up to 2 s to return before ncclCommAbort frees the
+    // communicator -- a call blocked longer is what the abort is there to release.
     int abort() override {
-        int rc = BAGUA_OK;
-        if (comm_) rc = nccl_status(ncclCommAbort(comm_));
-        comm_ = nullptr;
-        return rc;
+        if (aborted_.exchange(true)) return BAGUA_OK;
+        const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(2);
+        while (inflight_.load() > 0 && std::chrono::steady_clock::now() < until)
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        return comm_ ? nccl_status(ncclCommAbort(comm_)) : BAGUA_OK;
     }
 
    private:
+    struct Call {
+        explicit Call(RcclTransport* t) : t_(t) {
+            t_->inflight_.fetch_add(1);
+            ok = !t_->aborted_.load() && t_->comm_;
+        }
+        ~Call() { t_->inflight_.fetch_sub(1); }
+        RcclTransport* t_;
+        bool ok = false;
+    };
     ncclComm_t comm_;
+    std::atomic<bool> aborted_{false};
+    std::atomic<int> inflight_{0};
 };
 
 Transport* make_rccl_transport(ncclComm_t comm) { return new RcclTransport(comm); }
+
+static int32_t env_i32(const char* name, int32_t dflt) {
+    const char* v = std::getenv(name);
+    return v && *v ? (int32_t)std::strtol(v, nullptr, 10) : dflt;
+}
+
+ScheduleConfig read_schedule_config() {
+    ScheduleConfig c;
+    c.pieces_cap = env_i32("BAGUA_PIPELINE_PIECES", c.pieces_cap);
+    c.min_piece = env_i32("BAGUA_PIPELINE_MIN_PIECE", c.min_piece);
+    c.taper = env_i32("BAGUA_PIPELINE_TAPER", 0) == 1;
+    c.multipath = env_i32("BAGUA_RING_MULTIPATH", 0) != 0;
+    c.check = env_i32("BAGUA_CHECK_SCHEDULE", 0) != 0;
+    return c;
+}
+
+// Every rank adopts rank 0's schedule switches: an allgather of each rank's
+// ScheduleConfig on `stream` (the communicator's first collective, posted by every
+// rank inside creation), a warning naming the ranks whose environment differed.
+static int agree_schedule_config(Transport* t, size_t rank, size_t nranks, int device, hipStream_t stream,
+                                 ScheduleConfig* cfg) {
+    if (nranks <= 1) return BAGUA_OK;
+    const size_t one = sizeof(ScheduleConfig);
+    PoolBuffer buf;
+    int rc = buf.allocate(device, one * nranks);
+    if (rc) return rc;
+    std::vector<ScheduleConfig> all(nranks);
+    uint8_t* base = buf.as<uint8_t>();
+    if (hipMemcpyAsync(base + rank * one, cfg, one, hipMemcpyHostToDevice, stream) != hipSuccess) return BAGUA_ERR_HIP;
+    if ((rc = t->allgather(base + rank * one, base, one, BAGUA_DTYPE_U8, stream)) != BAGUA_OK) return rc;
+    if (hipMemcpyAsync(all.data(), base, one * nranks, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+        return BAGUA_ERR_HIP;
+    for (size_t r = 1; r < nranks; ++r)
+        if (!(all[r] == all[0]) && rank == 0)
+            BAGUA_LOG(1, "rank %zu's schedule environment (BAGUA_PIPELINE_*, BAGUA_RING_MULTIPATH, "
+                         "BAGUA_CHECK_SCHEDULE) differs from rank 0's; every rank uses rank 0's", r);
+    *cfg = all[0];
+    return BAGUA_OK;
+}
 
 }  // namespace bagua
 
@@ -144,6 +213,7 @@ BaguaSingleCommunicatorC* BaguaSingleCommunicatorC::lane(int i) {
         v->own_stream = true;
         v->parent = this;
         v->async = async;
+        v->cfg = cfg;
         v->aborted.store(aborted.load());
         // lanes run codec work beside each other: no one-launch encode (it needs every CU)
         (void)bagua_minmax_u8_set_stream_resident(s, 0);
@@ -188,6 +258,14 @@ BaguaSingleCommunicatorC* bagua_single_communicator_c_create(size_t rank, size_t
     c->nranks = nranks;
     c->device_id = (int)device_id;
     c->stream = (hipStream_t)(uintptr_t)stream_ptr;
+    c->cfg = read_schedule_config();
+    if (agree_schedule_config(c->t, rank, nranks, c->device_id, c->stream, &c->cfg) != BAGUA_OK) {
+        BAGUA_LOG(0, "communicator rank %zu/%zu: could not agree on the schedule switches", rank, nranks);
+        c->t->abort();
+        delete c->t;
+        delete c;
+        return nullptr;
+    }
     BAGUA_LOG(3, "communicator rank %zu/%zu on device %zu ready", rank, nranks, device_id);
     return c;
 }
@@ -232,6 +310,16 @@ int bagua_comm_abort(BaguaSingleCommunicatorC* c) {
 }
 
 int bagua_comm_check_abort(BaguaSingleCommunicatorC* c) { return c && c->aborted.load() ? 1 : 0; }
+
+int bagua_comm_schedule_config(BaguaSingleCommunicatorC* c, int32_t* out, int n) {
+    if (!c || !out || n < 5) return BAGUA_ERR_INVALID_ARG;
+    out[0] = c->cfg.pieces_cap;
+    out[1] = c->cfg.min_piece;
+    out[2] = c->cfg.taper;
+    out[3] = c->cfg.multipath;
+    out[4] = c->cfg.check;
+    return BAGUA_OK;
+}
 
 int bagua_comm_allreduce_inplace(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, int op) {
     // communicators/mod.rs:1020-1043 (count = num_elements_allocated)

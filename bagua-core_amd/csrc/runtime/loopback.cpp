@@ -11,6 +11,15 @@
 // posting order).  It exists so the comm ops (comm_ops.cpp) — the same code
 // that runs over RCCL on an 8-GPU node — are parity-tested at p > 1 on a
 // one-GPU box.  Barriers time out (60 s) instead of hanging.
+//
+// Every collective also publishes what it is (kind, bytes, root, op, this rank's
+// collective sequence number) beside its pointer; after the barrier every rank
+// compares all of them, and grouped send/recv compares every (sender, receiver)
+// pair's posted sizes.  Ranks that posted different collectives -- different piece
+// schedules, one rank in the ring op and another in the centralized one -- all
+// return BAGUA_ERR_COMM (after one more barrier, so nobody republishes while a peer
+// still reads) instead of copying past a buffer's end.  abort() breaks the group:
+// a rank waiting for a peer that never comes returns at once.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -31,16 +40,42 @@ struct Post {
     size_t bytes;
 };
 
+enum CollKind { kAllToAll = 1, kAllGather, kBroadcast, kAllReduce, kReduce, kP2P };
+
+// what a rank's current collective is; every rank's must be equal
+struct CollDesc {
+    int kind = 0, root = 0, op = 0;
+    size_t bytes = 0;
+    uint64_t seq = 0;
+    bool operator==(const CollDesc& o) const {
+        return kind == o.kind && root == o.root && op == o.op && bytes == o.bytes && seq == o.seq;
+    }
+};
+
+const char* kind_name(int k) {
+    static const char* n[] = {"?", "alltoall", "allgather", "broadcast", "allreduce", "reduce", "send/recv"};
+    return k >= 0 && k <= kP2P ? n[k] : "?";
+}
+
 struct LoopbackGroup {
-    explicit LoopbackGroup(int n, int dev) : p(n), device(dev), ptr(n), sends(n), recvs(n) {}
+    explicit LoopbackGroup(int n, int dev)
+        : p(n), device(dev), cfg(read_schedule_config()), ptr(n), desc(n), sends(n), recvs(n) {}
     int p, device;
+    ScheduleConfig cfg;  // one process: every virtual rank reads the same environment, once
     std::mutex mu;
     std::condition_variable cv;
     int arrived = 0;
     uint64_t gen = 0;
     bool broken = false;
     std::vector<const void*> ptr;            // per-rank published pointer
+    std::vector<CollDesc> desc;              // per-rank published collective
     std::vector<std::vector<Post>> sends, recvs;
+
+    void break_all() {
+        std::lock_guard<std::mutex> lk(mu);
+        broken = true;
+        cv.notify_all();
+    }
 
     bool barrier() {
         std::unique_lock<std::mutex> lk(mu);
@@ -67,14 +102,14 @@ class LoopbackTransport final : public Transport {
 
     int alltoall(const void* s, void* rcv, size_t n, int d, hipStream_t st) override {
         const size_t b = n * bagua_dtype_bytes(d);
-        if (!enter(st, s)) return BAGUA_ERR_COMM;
+        if (int rc = enter(st, s, kAllToAll, b)) return rc;
         for (int j = 0; j < g_->p; ++j)
             if (copy((uint8_t*)rcv + j * b, (const uint8_t*)g_->ptr[j] + r_ * b, b, st)) return BAGUA_ERR_HIP;
         return leave(st);
     }
     int allgather(const void* s, void* rcv, size_t n, int d, hipStream_t st) override {
         const size_t b = n * bagua_dtype_bytes(d);
-        if (!enter(st, s)) return BAGUA_ERR_COMM;
+        if (int rc = enter(st, s, kAllGather, b)) return rc;
         for (int j = 0; j < g_->p; ++j) {
             uint8_t* dst = (uint8_t*)rcv + j * b;
             if (dst == g_->ptr[j]) continue;  // in place
@@ -84,7 +119,7 @@ class LoopbackTransport final : public Transport {
     }
     int broadcast(void* buf, size_t n, int d, int root, hipStream_t st) override {
         const size_t b = n * bagua_dtype_bytes(d);
-        if (!enter(st, buf)) return BAGUA_ERR_COMM;
+        if (int rc = enter(st, buf, kBroadcast, b, root)) return rc;
         if (r_ != root && copy(buf, g_->ptr[root], b, st)) return BAGUA_ERR_HIP;
         return leave(st);
     }
@@ -94,7 +129,7 @@ class LoopbackTransport final : public Transport {
         const size_t b = n * bagua_dtype_bytes(d);
         PoolBuffer acc;
         if (acc.allocate(g_->device, b ? b : 1)) return BAGUA_ERR_OOM;
-        if (!enter(st, s)) return BAGUA_ERR_COMM;
+        if (int rc = enter(st, s, kAllReduce, b, 0, op)) return rc;
         if (copy(acc.as<void>(), g_->ptr[0], b, st)) return BAGUA_ERR_HIP;
         for (int j = 1; j < g_->p; ++j)
             if (bagua_add_inplace(d, acc.as<void>(), g_->ptr[j], (int)n, st)) return BAGUA_ERR_HIP;
@@ -109,7 +144,7 @@ class LoopbackTransport final : public Transport {
         const size_t b = n * bagua_dtype_bytes(d);
         PoolBuffer acc;
         if (r_ == root && acc.allocate(g_->device, b ? b : 1)) return BAGUA_ERR_OOM;
-        if (!enter(st, s)) return BAGUA_ERR_COMM;
+        if (int rc = enter(st, s, kReduce, b, root, op)) return rc;
         if (r_ == root) {
             if (copy(acc.as<void>(), g_->ptr[0], b, st)) return BAGUA_ERR_HIP;
             for (int j = 1; j < g_->p; ++j)
@@ -138,15 +173,42 @@ class LoopbackTransport final : public Transport {
         in_group_ = false;
         return flush(stream_);
     }
-    int abort() override { return BAGUA_OK; }
+    int abort() override {
+        g_->break_all();
+        return BAGUA_OK;
+    }
 
     void set_stream(hipStream_t s) { stream_ = s; }
 
    private:
-    bool enter(hipStream_t st, const void* publish) {
-        if (hipStreamSynchronize(st) != hipSuccess) return false;
+    // publish this rank's pointer and collective, wait for every rank, compare
+    int enter(hipStream_t st, const void* publish, int kind, size_t bytes, int root = 0, int op = 0) {
+        if (hipStreamSynchronize(st) != hipSuccess) return BAGUA_ERR_HIP;
         g_->ptr[r_] = publish;
-        return g_->barrier();
+        CollDesc me;
+        me.kind = kind;
+        me.bytes = bytes;
+        me.root = root;
+        me.op = op;
+        me.seq = seq_++;
+        g_->desc[r_] = me;
+        if (!g_->barrier()) return BAGUA_ERR_COMM;
+        for (int j = 0; j < g_->p; ++j)
+            if (!(g_->desc[j] == g_->desc[0])) {
+                if (r_ == 0)
+                    BAGUA_LOG(0, "loopback: collective mismatch, rank 0 posted %s of %zu bytes (#%llu), rank %d "
+                                 "%s of %zu bytes (#%llu)", kind_name(g_->desc[0].kind), g_->desc[0].bytes,
+                              (unsigned long long)g_->desc[0].seq, j, kind_name(g_->desc[j].kind), g_->desc[j].bytes,
+                              (unsigned long long)g_->desc[j].seq);
+                return mismatch();
+            }
+        return BAGUA_OK;
+    }
+    // every rank saw the same mismatch: one more barrier (nobody republishes while a
+    // peer is still comparing), then all fail alike
+    int mismatch() {
+        (void)g_->barrier();
+        return BAGUA_ERR_COMM;
     }
     int leave(hipStream_t st) {
         if (hipStreamSynchronize(st) != hipSuccess) return BAGUA_ERR_HIP;
@@ -161,27 +223,45 @@ class LoopbackTransport final : public Transport {
         if (hipStreamSynchronize(st) != hipSuccess) return BAGUA_ERR_HIP;
         g_->sends[r_] = my_sends_;
         g_->recvs[r_] = my_recvs_;
-        if (!g_->barrier()) return BAGUA_ERR_COMM;
-        std::vector<int> taken(g_->p, 0);  // k-th receive from q matches q's k-th send to me
-        for (const Post& rv : my_recvs_) {
+        my_sends_.clear();
+        my_recvs_.clear();
+        if (int rc = enter(st, nullptr, kP2P, 0)) return rc;
+        // every pair's posted sizes must agree: the k-th receive rank r posts from q has
+        // the size of the k-th send q posts to r, and nothing is left unmatched (every
+        // rank checks every pair, so all reach the same verdict)
+        const int p = g_->p;
+        for (int r = 0; r < p; ++r)
+            for (int q = 0; q < p; ++q) {
+                std::vector<size_t> sent, got;
+                for (const Post& sd : g_->sends[q])
+                    if (sd.peer == r) sent.push_back(sd.bytes);
+                for (const Post& rv : g_->recvs[r])
+                    if (rv.peer == q) got.push_back(rv.bytes);
+                if (sent != got) {
+                    if (r_ == 0)
+                        BAGUA_LOG(0, "loopback: send/recv mismatch, rank %d posts %zu sends to rank %d, which posts "
+                                     "%zu receives from it (or their sizes differ)", q, sent.size(), r, got.size());
+                    return mismatch();
+                }
+            }
+        std::vector<int> taken(p, 0);  // k-th receive from q matches q's k-th send to me
+        for (const Post& rv : g_->recvs[r_]) {
             int seen = 0;
             const Post* match = nullptr;
             for (const Post& sd : g_->sends[rv.peer]) {
                 if (sd.peer != r_) continue;
                 if (seen++ == taken[rv.peer]) { match = &sd; break; }
             }
-            if (!match || match->bytes != rv.bytes) return BAGUA_ERR_COMM;
             ++taken[rv.peer];
             if (copy(rv.ptr, match->ptr, rv.bytes, st)) return BAGUA_ERR_HIP;
         }
-        my_sends_.clear();
-        my_recvs_.clear();
         return leave(st);
     }
 
     LoopbackGroup* g_;
     int r_;
     bool in_group_ = false;
+    uint64_t seq_ = 0;  // collectives this rank posted
     hipStream_t stream_ = nullptr;
     std::vector<Post> my_sends_, my_recvs_;
 };
@@ -211,6 +291,7 @@ BaguaSingleCommunicatorC* bagua_loopback_communicator_create(void* group, size_t
     c->nranks = (size_t)g->p;
     c->device_id = g->device;
     c->stream = (hipStream_t)(uintptr_t)stream_ptr;
+    c->cfg = g->cfg;
     return c;
 }
 

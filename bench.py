@@ -26,6 +26,10 @@ host's cores on a bounded sample.
 """
 from __future__ import annotations
 
+import time as _time
+
+_PROCESS_T0 = _time.perf_counter()  # the N > 1 line's phase clock starts here (phase_wall_s)
+
 import argparse
 import ctypes
 import json
@@ -180,6 +184,31 @@ def parse():
     ap.add_argument("--stream", choices=["own", "current"], default="own",
                     help="codec workloads: launch on a stream of their own or on torch's current (null) stream")
     return ap.parse_args()
+
+
+class PhaseClock:
+    """Wall seconds per phase of a line (this rank's clock), from the process start on, so a
+    node run says where its time went (phase_wall_s; the phases sum to the process wall at
+    the moment the line is printed)."""
+
+    def __init__(self):
+        self.t = _PROCESS_T0
+        self.s = {}
+
+    def lap(self, name: str) -> None:
+        now = time.perf_counter()
+        self.s[name] = self.s.get(name, 0.0) + (now - self.t)
+        self.t = now
+
+    def report(self) -> dict:
+        total = time.perf_counter() - _PROCESS_T0
+        out = {k: round(v, 3) for k, v in self.s.items()}
+        out["unaccounted"] = round(total - sum(self.s.values()), 3)
+        out["process_wall"] = round(total, 3)
+        return out
+
+
+PHASES = PhaseClock()
 
 
 def pmc_traffic(kernel: str, summary: str = PMC_SUMMARY):
@@ -718,6 +747,7 @@ def allreduce_p1(args, n: int = 1 << 28):
 
 # ----------------------------------------------------------------- N > 1 ------
 def bench_allreduce(args, world: int, rank: int, local_rank: int):
+    PHASES.lap("startup")  # interpreter, torch import, argument parsing
     import torch.distributed as dist
     from bagua_core import BaguaSingleCommunicatorPy, BaguaTensorPy
     from bagua_core import _native as N
@@ -741,6 +771,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     x = torch.randn(n, device=dev, generator=g) * 1e-3
     torch.cuda.synchronize()
     raw = BaguaTensorPy(x, "gradient_bucket").raw()
+    PHASES.lap("setup")  # process group, RCCL communicator, 1 GiB bucket
 
     headline_taper = [False]  # the autotune may pick tapered pieces (N.PIECES_TAPERED) for the headline
 
@@ -842,6 +873,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             best = min(autotune, key=lambda q: autotune[q])
             args.pieces = int(best.split("_")[0])
             headline_taper[0] = best.endswith("_tapered")
+            PHASES.lap("autotune")
         t_c = timed(compressed_step, args.steps, args.warmup)
         err = "timed out; communicator aborted" if aborted else None
     except Exception as e:  # noqa: BLE001 - an op error on every rank alike
@@ -860,7 +892,9 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         comm = make_comm()
         args.pieces = 1
         t_c = timed(lambda: compressed_step(1), args.steps, args.warmup)
+    PHASES.lap("headline")
     t_u = side("unpieced", lambda: compressed_step(1))
+    PHASES.lap("unpieced")
     # piece counts either side of the automatic choice (4 per chunk at 1 GiB), so the node's own
     # run says which count hides the codec best behind its links
     sweep = {}
@@ -874,7 +908,9 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
 
         for q in (4, 5):
             sweep[f"{q}_tapered"] = side(f"pieces_{q}_tapered", lambda q=q: tapered(q))
+        PHASES.lap("pieces_sweep")
     t_f = side("fp32_allreduce", fp32_step)
+    PHASES.lap("fp32_allreduce")
     # the same all-reduce with the 1-bit sign+scale codec (this repo's extension:
     # N/8 wire bytes per phase instead of N), fused middle step
     def onebit_step(pieces=user_pieces):
@@ -895,6 +931,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
 
     t_comm = side("comm_only", comm_only)
     del cbuf, craw
+    PHASES.lap("comm_only")
     # Bagua's default bucket size (25 MiB of fp32): the same op and the fp32 all-reduce on the
     # first 25 MiB of the bucket, where latency, not bandwidth, sets the step
     m = min(n, (25 << 20) // 4)
@@ -904,6 +941,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         comm.handle, ctypes.byref(small), 1, N.COMPRESSION_MINMAX_UINT8, user_pieces), "25 MiB op"))
     t_sf = side("bucket_25mib_fp32", lambda: N.check(N.C.bagua_centralized_full_precision_synchronous(
         comm.handle, ctypes.byref(small), 1), "25 MiB fp32 allreduce"))
+    PHASES.lap("bucket_25mib")
     # the scheduler workload (32 x 25 MiB buckets, Bagua's default bucket size) through the native
     # scheduler on this communicator: cross-bucket lanes (the default) and one lane, so the node's
     # run shows how much of each bucket's codec prefix the next bucket's exchange hides
@@ -923,8 +961,10 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             del wl
         except Exception as e:  # noqa: BLE001 - a failed side measurement must not lose the headline line
             side_errors.setdefault("scheduler", str(e)[:200])
+        PHASES.lap("scheduler_buckets")
     t_o = side("onebit", onebit_step)
     t_ou = side("onebit_unpieced", lambda: onebit_step(1))
+    PHASES.lap("onebit")
     decentralized = None
     if not args.no_decentralized:
         # config 5: bf16 bucket, decentralized ring exchange with the uint8 codec
@@ -955,6 +995,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             del bufs, draws
         except Exception as e:  # noqa: BLE001 - a failed side measurement must not lose the headline line
             decentralized = {"error": str(e)[:200]}
+        PHASES.lap("decentralized_bf16")
     value = world * 4.0 * n / t_c / GiB
     per_rank = 4.0 * n / t_c / GiB
     fp32 = 4.0 * n / t_f / GiB
@@ -996,6 +1037,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             # the committed PMC pass is of the 256 MiB codec launch; at this size: unmeasured
             "traffic": pmc_traffic(names[dom]) if n == (1 << 26) and world == 1 else None,
             "alg_bytes_per_launch": alg[dom], "avg_launch_us": round(per[dom] * 1e3, 2)}
+    PHASES.lap("roofline")
     cfg = {"workload": f"minmax_uint8_compressed_allreduce_{4 * n >> 20}MiB_fp32_per_rank", "bucket_elements": n,
            "n_chunks": world, "collectives": "rccl alltoall + allgather (uint8)", "parallelism": f"dp{world}",
            "config_index": 4}
@@ -1199,7 +1241,13 @@ def main():
         # after every rank's timed region: rank 0 times the op on the host cores while
         # the others wait at the closing barrier
         if rank == 0 and not args.no_cpu_baseline:
-            cpu = cpu_allreduce_baseline(args, world, n_cpu, torch.device("cuda", local_rank))
+            try:
+                cpu = cpu_allreduce_baseline(args, world, n_cpu, torch.device("cuda", local_rank))
+            except Exception as e:  # noqa: BLE001 - a failed baseline must not lose the headline line
+                cpu = {"error": str(e)[:200]}
+            PHASES.lap("cpu_baseline")
+        if workload == "allreduce":
+            extra["phase_wall_s"] = PHASES.report()
         dtype = "f32 -> u8"
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,

@@ -117,6 +117,14 @@ uint64_t bagua_single_communicator_c_stream(BaguaSingleCommunicatorC* comm);
 int bagua_generate_nccl_unique_id_str(char* buf, size_t buf_len);
 int bagua_comm_abort(BaguaSingleCommunicatorC* comm);
 int bagua_comm_check_abort(BaguaSingleCommunicatorC* comm);
+/* The switches that shape an op's collectives, fixed when the communicator is created
+ * and equal on every rank (rank 0's environment wins; an op never reads them again):
+ * out[0..4] = BAGUA_PIPELINE_PIECES (piece cap), BAGUA_PIPELINE_MIN_PIECE,
+ * BAGUA_PIPELINE_TAPER, BAGUA_RING_MULTIPATH, BAGUA_CHECK_SCHEDULE.  With the last on,
+ * every op first allgathers a descriptor of itself (op, codec, dtype, p, chunk size,
+ * tensor sizes, piece schedule, average, op number) and all ranks return
+ * BAGUA_ERR_INVALID_ARG, before posting anything, when any two differ. */
+int bagua_comm_schedule_config(BaguaSingleCommunicatorC* comm, int32_t* out, int n);
 int bagua_comm_allreduce_inplace(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* t, int op);
 int bagua_comm_allreduce(BaguaSingleCommunicatorC* comm, const bagua_tensor_t* send, const bagua_tensor_t* recv,
                          int op);
@@ -303,8 +311,17 @@ int bagua_comm_backend_mark_communication_ready_desc(BaguaCommBackendC* backend,
                                                     uint64_t ready_event, const bagua_tensor_t* current);
 /* lib.rs:321-337: *completed = ops waited for; returns the first failure's status */
 int bagua_comm_backend_wait_pending_comm_ops(BaguaCommBackendC* backend, int* completed);
-/* ops the monitor saw running longer than 300 s (lib.rs:255-265) */
+/* The monitor (lib.rs:255-265): an op whose work has not completed 300 s after the
+ * worker picked it up (BAGUA_COMM_OP_TIMEOUT_S, or set_op_timeout_ms) is failed: its
+ * message is kept, its communicators are aborted (bagua_comm_abort: ncclCommAbort
+ * releases RCCL kernels waiting for an absent peer) and wait_pending_comm_ops
+ * returns BAGUA_ERR_ABORTED instead of blocking.  The reference panics the process
+ * instead (py/lib.rs:498-504).  failures = how many ops failed this way;
+ * failure_message copies message i into buf (NUL-terminated, truncated to len) and
+ * returns its full length, -1 when there is no message i. */
 int bagua_comm_backend_failures(BaguaCommBackendC* backend);
+int bagua_comm_backend_failure_message(BaguaCommBackendC* backend, int i, char* buf, size_t len);
+int bagua_comm_backend_set_op_timeout_ms(BaguaCommBackendC* backend, int64_t ms);
 /* Cross-bucket pipelining (no reference counterpart): bucket i of the registration
  * order runs on lane 1 + i % lanes of its communicator -- a view with its own
  * streams -- so consecutive buckets overlap on the GPU; 1 = every bucket on the

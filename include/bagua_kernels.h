@@ -210,6 +210,17 @@ int bagua_minmax_u8_reduce_requantize_final(int dtype, const uint8_t* input, siz
 int bagua_minmax_u8_centralized_one_rank(int dtype, void* tensor, int num_elem, int average, void* workspace,
                                          size_t workspace_bytes, bagua_stream_t stream);
 
+/* The same for the 1-bit codec (this repository's extension): at one
+ * rank the fused middle step's table has two entries (the reduced value of a 0 and
+ * of a 1 sign bit, equal in magnitude), so the op is the encode pass (sign bits +
+ * |x| tile partials), one workgroup deriving the first scale, the two reduced values
+ * and the second scale through the encoder's fixed tree, and one pass writing
+ * +-scale2 from the bits.  Bit-identical to the op's sequence; every element valid.
+ * Workspace: bagua_onebit_one_rank_workspace_bytes(num_elem), 16-B aligned. */
+size_t bagua_onebit_one_rank_workspace_bytes(int num_elem);
+int bagua_onebit_centralized_one_rank(int dtype, void* tensor, int num_elem, int average, void* workspace,
+                                      size_t workspace_bytes, bagua_stream_t stream);
+
 /* Pipelined all-reduce building blocks (no reference counterpart: the same
  * kernels restricted to part of every chunk, so communication of one piece
  * overlaps the codec work of the next).  A chunk splits into `pieces` element

@@ -112,9 +112,9 @@ def main() -> None:
             torch.cuda.synchronize()  # the reset (current stream) lands before the next op (comm stream)
         comm.barrier()
     elif scenario == "decentralized":
-        comm = comm_of("all", rank, world, rank == 0)
-        if "multipath" in kw:
+        if "multipath" in kw:  # read when the communicator is created (rank 0's value wins)
             os.environ["BAGUA_RING_MULTIPATH"] = kw["multipath"]
+        comm = comm_of("all", rank, world, rank == 0)
         ts = [_dev(inputs[f"{k}{rank}"], dtype) for k in "twlr"]
         raws = [bc.BaguaTensorPy(x, k).raw() for x, k in zip(ts, "twlr")]
         pieces = int(kw.get("pieces", 0))
@@ -151,22 +151,103 @@ def main() -> None:
             tensors.append(ts)
             buckets.append(bk)
         backend = bc.BaguaCommBackendPy(nb, 0)
+        lanes = int(kw.get("lanes", 0))
+        if lanes:
+            backend.set_lanes(lanes)
         backend.register_ordered_buckets(list(reversed(buckets)))
-        # the ready events must outlive the scheduled executions that wait for them (the
-        # scheduler keeps the raw handle, as the reference's BaguaTensor does)
-        events = []
-        for b in reversed(range(nb)):
-            ev = torch.cuda.Event()
-            ev.record()
-            events.append(ev)
-            for t in tensors[b]:
-                backend.mark_communication_ready(t, ev.cuda_event)
-        done = backend.wait_pending_comm_ops()
-        del events
-        assert done == nb, done
+        # `steps` back-to-back steps, each bucket's output the next step's input (with
+        # several lanes, consecutive buckets run on different streams of ONE RCCL
+        # communicator: their collectives must still pair up in issue order on every rank)
+        for step in range(int(kw.get("steps", 1))):
+            # the ready events must outlive the scheduled executions that wait for them (the
+            # scheduler keeps the raw handle, as the reference's BaguaTensor does)
+            events = []
+            for b in reversed(range(nb)):
+                ev = torch.cuda.Event()
+                ev.record()
+                events.append(ev)
+                for t in tensors[b]:
+                    backend.mark_communication_ready(t, ev.cuda_event)
+            done = backend.wait_pending_comm_ops()
+            del events
+            assert done == nb, done
         out = {f"b{b}": _host(f) for b, f in enumerate(flats)}
+        out["lanes"] = np.array([backend.lanes()])
         comm.barrier()
         del backend
+    elif scenario == "mismatch":
+        # ranks posting different op schedules.  Rank 1's own environment tapers the pieces
+        # and rank 0's does not: rank 0's value must win at creation (else the first op
+        # below would post mismatched grouped send/recv and hang).  BAGUA_CHECK_SCHEDULE is
+        # set on rank 0 only -- it must reach rank 1 the same way.  Then rank 0 asks for 4
+        # pieces and rank 1 for 2: both must fail with invalid argument, tensors untouched,
+        # and the communicator must still run a matching op afterwards.
+        if rank == 0:
+            os.environ["BAGUA_CHECK_SCHEDULE"] = "1"
+        else:
+            os.environ["BAGUA_PIPELINE_TAPER"] = "1"
+        comm = comm_of("all", rank, world, rank == 0)
+        t = _dev(inputs[f"x{rank}"], F32)
+        raw = bc.BaguaTensorPy(t, "g").raw()
+        op = N.C.bagua_centralized_low_precision_pipelined
+        M = N.COMPRESSION_MINMAX_UINT8
+        rc_same = op(comm.handle, ctypes.byref(raw), 1, M, 5)  # 5 pieces: tapered only on rank 1's env
+        comm.synchronize()
+        out["same"] = _host(t)
+        t.copy_(_dev(inputs[f"x{rank}"], F32))
+        torch.cuda.synchronize()
+        rc_pieces = op(comm.handle, ctypes.byref(raw), 1, M, 4 if rank == 0 else 2)
+        comm.synchronize()
+        out["after_pieces"] = _host(t)
+        rc_kind = (op(comm.handle, ctypes.byref(raw), 1, M, 3) if rank == 0 else
+                   N.C.bagua_centralized_low_precision_synchronous_unfused(comm.handle, ctypes.byref(raw), 1, M))
+        comm.synchronize()
+        out["after_kind"] = _host(t)
+        rc_again = op(comm.handle, ctypes.byref(raw), 1, M, 3)
+        comm.synchronize()
+        out["again"] = _host(t)
+        out["rc"] = np.array([rc_same, rc_pieces, rc_kind, rc_again])
+        out["cfg"] = np.array(list(comm.schedule_config().values()))
+        comm.barrier()
+    elif scenario == "stuck":
+        # rank 1 never posts the op: rank 0's scheduler monitor must fail it after its
+        # limit, abort the communicator and let wait_pending_comm_ops raise
+        comm = comm_of("all", rank, world, rank == 0)
+        flag = os.path.join(workdir, "rank0_done")
+        if rank == 0:
+            x = _dev(inputs["x0"], F32)
+            bk = bc.BaguaBucketPy("stuck_bucket", [bc.BaguaTensorPy(x, "x")])
+            bk.append_centralized_synchronous_op(comm, None, False, True, False, "MinMaxUInt8")
+            backend = bc.BaguaCommBackendPy(1, 0)
+            limit = float(kw.get("limit", 3))
+            backend.set_op_timeout(limit)
+            backend.register_ordered_buckets([bk])
+            ev = torch.cuda.Event()
+            ev.record()
+            t0 = time.time()
+            backend.mark_communication_ready(bk.tensors()[0], ev.cuda_event)
+            msg = ""
+            try:
+                backend.wait_pending_comm_ops()
+            except RuntimeError as e:
+                msg = str(e)
+            elapsed = time.time() - t0
+            failures = backend.failures()
+            del backend  # must not hang on the aborted op
+            out = {"elapsed": np.array([elapsed]), "raised": np.array([bool(msg)]),
+                   "failures": np.array([len(failures)]), "aborted": np.array([comm.check_abort()])}
+            print(f"rank 0: wait_pending_comm_ops -> {msg!r} after {elapsed:.2f} s", flush=True)
+            with open(flag, "w") as f:
+                f.write("done")
+        else:
+            deadline = time.time() + 60
+            while not os.path.exists(flag) and time.time() < deadline:
+                time.sleep(0.05)
+            comm.abort()
+            out = {"peer": np.array([1])}
+        np.savez(os.path.join(workdir, f"out{rank}.npz"), **out)
+        print(f"rank {rank}/{world} {scenario} ok", flush=True)
+        os._exit(0)  # the aborted communicator is not torn down any further
     else:
         raise SystemExit(f"unknown scenario {scenario}")
     np.savez(os.path.join(workdir, f"out{rank}.npz"), **out)

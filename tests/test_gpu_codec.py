@@ -578,3 +578,72 @@ def test_one_rank_op_load_policy_split(bc, oracle_c, dtype, keep_mib, monkeypatc
     xt = to_dev(x, dtype, 0)
     assert K.bagua_minmax_u8_centralized_one_rank(dtype, xt.data_ptr(), n, 1, ws.data_ptr(), wsb, None) == 0
     assert_float_bits_equal(to_host(xt, dtype), want, dtype, f"one rank keep={keep_mib}")
+
+
+@pytest.mark.parametrize("dtype", [F32, F16, BF16])
+@pytest.mark.parametrize("case", ["normal", "ragged", "offset", "nan_mixed", "pos_inf", "both_inf", "all_nan",
+                                  "zeros", "neg_zeros", "constant", "huge", "tiny", "one"])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_onebit_one_rank_op_matches_sequence(bc, oracle_c, dtype, case, offset):
+    """bagua_onebit_centralized_one_rank (encode pass, one workgroup for both scales, one pass
+    writing +-scale2 from the bits) == the 1-bit op's sequence at p = 1 (encode, decode +
+    reduce + re-encode, decode; centralized_low_precision_synchronous.rs:30-71 with the
+    1-bit codec), bit for bit: regular, ragged last tile, +-0, NaN / Inf, overflowing
+    scale sums, tiny tensors; aligned and misaligned; mean and sum."""
+    from oracle import oracle_np as NP
+    from oracle import simulate
+    K = bc._native.K
+    rng = np.random.default_rng(len(case) * 11 + dtype + offset)
+    n = {"tiny": 5, "one": 1, "ragged": (1 << 20) + 37}.get(case, 1 << 20)
+    big = {F32: 3e38, F16: 6e4, BF16: 3e38}[dtype]
+    v = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+    if case == "offset":
+        v += 7.5
+    elif case == "nan_mixed":
+        v[::7] = np.nan
+    elif case == "pos_inf":
+        v[5] = np.inf
+    elif case == "both_inf":
+        v[3], v[4] = np.inf, -np.inf
+    elif case == "all_nan":
+        v[:] = np.nan
+    elif case == "zeros":
+        v[:] = 0.0
+    elif case == "neg_zeros":
+        v[:] = -0.0
+        v[::3] = 0.0
+    elif case == "constant":
+        v[:] = -0.25
+    elif case == "huge":
+        v[:] = big  # the |x| tree overflows to inf
+        v[1::2] = -big
+    x = NP.from_f32(v, dtype)
+    wsb = K.bagua_onebit_one_rank_workspace_bytes(n)
+    ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+    for average in (1, 0):
+        want = simulate.centralized_low_precision(oracle_c, [x.copy()], dtype, bool(average),
+                                                  method="OneBitSignScale")[0]
+        xt = to_dev(x, dtype, offset)
+        assert K.bagua_onebit_centralized_one_rank(dtype, xt.data_ptr(), n, average, ws.data_ptr(), wsb, None) == 0
+        assert_float_bits_equal(to_host(xt, dtype), want, dtype, f"1-bit one rank {case} average={average}")
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_onebit_one_rank_through_the_op(bc, oracle_c, fused, monkeypatch):
+    """The centralized op at one rank with the 1-bit codec takes the two-pass path
+    (BAGUA_ONE_RANK_FUSED=1, the default) or the full sequence (0): same bytes, the oracle's."""
+    from bagua_core.communicator import loopback_communicators
+    from oracle import simulate
+    monkeypatch.setenv("BAGUA_ONE_RANK_FUSED", fused)
+    N = bc._native
+    n = (1 << 21) + 1000
+    x = (np.random.default_rng(5).standard_normal(n) * 1e-3).astype(np.float32)
+    want = simulate.centralized_low_precision(oracle_c, [x.copy()], F32, True, method="OneBitSignScale")[0]
+    comm = loopback_communicators(1, 0)[0]
+    t = torch.from_numpy(x.copy()).cuda()
+    torch.cuda.synchronize()
+    raw = bc.BaguaTensorPy(t, "g").raw()
+    N.check(N.C.bagua_centralized_low_precision_synchronous(comm.handle, ctypes.byref(raw), 1, N.COMPRESSION_ONEBIT),
+            "1-bit op")
+    comm.synchronize()
+    assert_float_bits_equal(t.cpu().numpy(), want, F32, f"fused={fused}")

@@ -104,7 +104,7 @@ def test_centralized_onebit_allreduce_1gib_p8_properties():
 
 
 @pytest.mark.parametrize("multipath", ["0", "1"])
-def test_decentralized_ring_bf16_p8_full_size_properties(multipath):
+def test_decentralized_ring_bf16_p8_full_size_properties(multipath, monkeypatch):
     """Config 5 at full size (2^27 bf16 elements per rank, 8 ranks; the default direct
     exchange and the opt-in multipath one): with mix_r = t_r + (l_r + r_r) f13 + w_r f53 (f13, f53 =
     1/3 and -5/3 rounded to bf16 as the 16-bit addmul does; the bucket
@@ -134,6 +134,7 @@ def test_decentralized_ring_bf16_p8_full_size_properties(multipath):
     mag = [ts["t"][r].double().abs() + old["l"][r].abs() / 3 + old["r"][r].abs() / 3 + 5 * old["w"][r].abs() / 3
            for r in range(p)]
     step = [float((mx.max() - mx.min()) + 1e-7) / 255.0 for mx in mix]
+    monkeypatch.setenv("BAGUA_RING_MULTIPATH", multipath)  # read when the communicators are created
     comms = loopback_communicators(p, 0)
     torch.cuda.synchronize()
 
@@ -142,17 +143,8 @@ def test_decentralized_ring_bf16_p8_full_size_properties(multipath):
         N.check(N.C.bagua_decentralized_low_precision_synchronous(comms[r].handle, *[ctypes.byref(x) for x in raws],
                                                                   N.COMPRESSION_MINMAX_UINT8), f"rank {r}")
 
-    import os
-    old_env = os.environ.get("BAGUA_RING_MULTIPATH")
-    os.environ["BAGUA_RING_MULTIPATH"] = multipath
-    try:
-        run_ranks(rank, p)
-        torch.cuda.synchronize()
-    finally:
-        if old_env is None:
-            os.environ.pop("BAGUA_RING_MULTIPATH", None)
-        else:
-            os.environ["BAGUA_RING_MULTIPATH"] = old_env
+    run_ranks(rank, p)
+    torch.cuda.synchronize()
     for r in range(p):
         t_new = ts["t"][r].double()
         assert torch.equal(ts["w"][r].view(torch.int16), ts["t"][r].view(torch.int16)), f"rank {r}: w != t"

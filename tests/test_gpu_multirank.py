@@ -324,35 +324,29 @@ def test_pipelined_ops_back_to_back_fuzz(bc, oracle_c):
                                                        (8, F32, 65536 + 7, 0, True), (7, F16, 40000, 3, True),
                                                        (12, BF16, 20000, 2, True), (8, BF16, 70001, 4, False),
                                                        (8, F32, (1 << 20) + 3, 4, True)])
-def test_decentralized_multipath_multirank(bc, oracle_c, p, dtype, n, pieces, multipath):
+def test_decentralized_multipath_multirank(bc, oracle_c, p, dtype, n, pieces, multipath, monkeypatch):
     """Ring op with the multipath exchange (from 6 ranks: 3/p of each piece straight to the
     peer, the other slices relayed through ranks r +- (k-1) one group later; comm_ops.cpp
     ring_ops) == the oracle's op simulation on every rank and tensor; multipath False
     (BAGUA_RING_MULTIPATH=0) is the reference's direct exchange."""
-    import os
     from bagua_core.communicator import loopback_communicators
     rng = np.random.default_rng(700 + p + n + pieces)
     arrs = {k: [NP.from_f32((rng.standard_normal(n) * 1e-3).astype(np.float32), dtype) for _ in range(p)]
             for k in "twlr"}
     want = simulate.decentralized_low_precision(oracle_c, arrs["t"], arrs["w"], arrs["l"], arrs["r"], dtype)
+    # read once, when the communicators are created (ScheduleConfig)
+    monkeypatch.setenv("BAGUA_RING_MULTIPATH", "1" if multipath else "0")
     comms = loopback_communicators(p, 0)
     dts = {k: [dev(a, dtype) for a in arrs[k]] for k in "twlr"}
     torch.cuda.synchronize()
     N = bc._native
-    old = os.environ.get("BAGUA_RING_MULTIPATH")
-    os.environ["BAGUA_RING_MULTIPATH"] = "1" if multipath else "0"
-    try:
-        def rank(r):
-            raws = [bc.BaguaTensorPy(dts[k][r], k).raw() for k in "twlr"]
-            N.check(N.C.bagua_decentralized_low_precision_pipelined(
-                comms[r].handle, *[ctypes.byref(x) for x in raws], N.COMPRESSION_MINMAX_UINT8, pieces), f"rank {r}")
 
-        run_ranks(rank, p)
-    finally:
-        if old is None:
-            os.environ.pop("BAGUA_RING_MULTIPATH", None)
-        else:
-            os.environ["BAGUA_RING_MULTIPATH"] = old
+    def rank(r):
+        raws = [bc.BaguaTensorPy(dts[k][r], k).raw() for k in "twlr"]
+        N.check(N.C.bagua_decentralized_low_precision_pipelined(
+            comms[r].handle, *[ctypes.byref(x) for x in raws], N.COMPRESSION_MINMAX_UINT8, pieces), f"rank {r}")
+
+    run_ranks(rank, p)
     for k, wk in zip("twlr", want):
         for r in range(p):
             assert np.array_equal(host(dts[k][r], dtype).view(np.uint8), wk[r].view(np.uint8)), f"{k} rank {r}"

@@ -211,6 +211,10 @@ def test_bench_line_multirank(tmp_path, world, fail_headline, launcher):
     c = d["cpu_baseline"]
     assert c and c["value"] > 0 and c["cores"] >= 1 and c["host"]["os_cpu_count"] >= 1 and str(world) in c["sample"]
     assert d["hw_queues"]["effective"] == "8", d["hw_queues"]
+    ph = d["phase_wall_s"]  # where the line's wall time went, phase by phase (rank 0's clock)
+    for k in ("startup", "setup", "headline", "fp32_allreduce", "scheduler_buckets", "onebit", "cpu_baseline"):
+        assert ph[k] >= 0, (k, ph)
+    assert abs(ph["unaccounted"]) <= 0.05 * ph["process_wall"], ph
 
 
 def test_native_scheduler(tmp_path, oracle_c):
@@ -222,3 +226,59 @@ def test_native_scheduler(tmp_path, oracle_c):
         want = simulate.centralized_low_precision(oracle_c, [xs[(b, r)] for r in range(world)], F32, True)
         for r in range(world):
             assert np.array_equal(outs[r][f"b{b}"], want[r].view(np.uint8)), (b, r)
+
+
+@pytest.mark.parametrize("lanes,steps,nb", [(1, 2, 7), (3, 2, 7)])
+def test_native_scheduler_lanes_over_rccl(tmp_path, oracle_c, lanes, steps, nb):
+    """Scheduler lanes over a real RCCL communicator: with 3 lanes, consecutive buckets'
+    collectives go out on different streams of ONE ncclComm, and stay correct only because
+    RCCL runs a communicator's operations in the order they are issued, whatever the stream
+    (every rank's scheduler worker issues them in the same order).  7 buckets over 2 steps,
+    each step's output feeding the next: every bucket's bytes equal the oracle's two
+    applications of the reference op, with 3 lanes and with 1."""
+    world, per = 2, 2 * 8192
+    rng = np.random.default_rng(90 + lanes)
+    xs = {(b, r): (rng.standard_normal(per) * 1e-3).astype(np.float32) for b in range(nb) for r in range(world)}
+    outs = run_procs(tmp_path, "backend", world, {f"b{b}_{r}": x for (b, r), x in xs.items()}, buckets=nb,
+                     lanes=lanes, steps=steps)
+    for r in range(world):
+        assert int(outs[r]["lanes"][0]) == lanes
+    for b in range(nb):
+        want = [xs[(b, r)] for r in range(world)]
+        for _ in range(steps):
+            want = simulate.centralized_low_precision(oracle_c, want, F32, True)
+        for r in range(world):
+            assert np.array_equal(outs[r][f"b{b}"], want[r].view(np.uint8)), (b, r)
+
+
+def test_schedule_mismatch_over_rccl(tmp_path, oracle_c):
+    """Rank 0's schedule switches win at creation (rank 1's own BAGUA_PIPELINE_TAPER is
+    ignored, rank 0's BAGUA_CHECK_SCHEDULE reaches rank 1); with the check on, ranks asking
+    for different piece counts, or one the pipelined op and the other the unfused one, all
+    fail with invalid argument before posting anything, tensors untouched, and the same
+    communicator then runs a matching op bit-exactly."""
+    world, cs = 2, 4 * 16384
+    rng = np.random.default_rng(515)
+    xs = [(rng.standard_normal(world * cs) * 1e-3).astype(np.float32) for _ in range(world)]
+    want = simulate.centralized_low_precision(oracle_c, xs, F32, True)
+    outs = run_procs(tmp_path, "mismatch", world, {f"x{r}": x for r, x in enumerate(xs)})
+    for r, o in enumerate(outs):
+        assert o["rc"].tolist() == [0, 1, 1, 0], (r, o["rc"])
+        assert o["cfg"].tolist() == [4, 1 << 20, 0, 0, 1], (r, o["cfg"])  # rank 0's switches on both
+        assert np.array_equal(o["same"], want[r].view(np.uint8)), r
+        assert np.array_equal(o["after_pieces"], xs[r].view(np.uint8)), r
+        assert np.array_equal(o["after_kind"], xs[r].view(np.uint8)), r
+        assert np.array_equal(o["again"], want[r].view(np.uint8)), r
+
+
+def test_stuck_op_fails_over_rccl(tmp_path):
+    """lib.rs:255-265 monitor: rank 1 never posts the op, so rank 0's alltoall waits for a
+    peer that never comes.  After the 3 s limit the monitor aborts rank 0's communicator
+    (ncclCommAbort), wait_pending_comm_ops raises within the limit plus a margin, and the
+    scheduler is destroyed without hanging."""
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal(2 * 65536) * 1e-3).astype(np.float32)
+    outs = run_procs(tmp_path, "stuck", 2, {"x0": x}, limit=3)
+    o = outs[0]
+    assert bool(o["raised"][0]) and int(o["failures"][0]) == 1 and bool(o["aborted"][0]), o
+    assert 3.0 <= float(o["elapsed"][0]) < 3.0 + 15.0, o["elapsed"]
