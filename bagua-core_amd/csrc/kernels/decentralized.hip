@@ -87,7 +87,7 @@ __device__ __forceinline__ float mix(float t, float l, float r, float w, float f
     return addmul<T>(t, w, f53);
 }
 
-template <typename T, int U, bool CONTIG = false>
+template <typename T, int U, bool CONTIG = false, bool NTS = false>
 __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* __restrict__ t,
                                                           const typename T::storage* __restrict__ l,
                                                           const typename T::storage* __restrict__ r,
@@ -111,8 +111,9 @@ __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* _
             lo = min(lo, min_space_key(k));
             hi = min(hi, max_space_key(k));
         }
-        // plain store: the quantise pass re-reads t next
-        reinterpret_cast<uint4*>(t)[v] = pack16<T>(ft);
+        // plain store: the quantise pass re-reads t next (NTS: non-temporal, A/B)
+        if constexpr (NTS) nt_store16(pack16<T>(ft), reinterpret_cast<uint4*>(t) + v);
+        else reinterpret_cast<uint4*>(t)[v] = pack16<T>(ft);
     };
     const uint4* t4 = reinterpret_cast<const uint4*>(t);
     const uint4* l4 = reinterpret_cast<const uint4*>(l);
@@ -332,15 +333,20 @@ static int mix_impl(void* t, const void* l, const void* r, const void* w, int n,
     if (!aligned16(t) || !aligned16(l) || !aligned16(r) || !aligned16(w)) return BAGUA_ERR_UNSUPPORTED;
     const int nblk = ws ? minmax_partials_blocks(n, Vec<T>::N, 1, ws_bytes) : 0;
     if (nblk < 1) return BAGUA_ERR_WORKSPACE;
-    const char* e = getenv("BAGUA_RING_MIX_CONTIG");  // A/B (tools/ring_apply_sweep.py)
-    if (e && e[0] == '1')
-        launch(ring_mix_kernel<T, kMixUnroll, true>, dim3(nblk), dim3(kBlock), 0, s, static_cast<S*>(t),
-               static_cast<const S*>(l), static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13, f53,
-               static_cast<uint2*>(ws));
-    else
-        launch(ring_mix_kernel<T, kMixUnroll>, dim3(nblk), dim3(kBlock), 0, s, static_cast<S*>(t),
-               static_cast<const S*>(l), static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13, f53,
-               static_cast<uint2*>(ws));
+    // A/B knobs (tools/kernel_ab.py --variants): contiguous ranges per workgroup, a
+    // non-temporal store of the mixed t.  (The grid stays nblk: the quantise pass folds
+    // exactly that many partials.)
+    const bool contig = tune_int("BAGUA_RING_MIX_CONTIG", 0) == 1;
+    const bool nts = tune_int("BAGUA_RING_MIX_NTS", 0) == 1;
+    const int grid = nblk;
+    auto go = [&](auto kern) {
+        launch(kern, dim3(grid), dim3(kBlock), 0, s, static_cast<S*>(t), static_cast<const S*>(l),
+               static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13, f53, static_cast<uint2*>(ws));
+    };
+    if (contig && nts) go(ring_mix_kernel<T, kMixUnroll, true, true>);
+    else if (contig) go(ring_mix_kernel<T, kMixUnroll, true, false>);
+    else if (nts) go(ring_mix_kernel<T, kMixUnroll, false, true>);
+    else go(ring_mix_kernel<T, kMixUnroll, false, false>);
     return check_launch();
 }
 

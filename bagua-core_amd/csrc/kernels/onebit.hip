@@ -196,6 +196,27 @@ __device__ __forceinline__ float tile_from(const float* v, int64_t base, int64_t
     return wave_tree_sum(lane_tree(a));
 }
 
+// Levels >= 2 of the chunk tree: lvl[0][0, ceil(m1 / 1024)) holds the level-1 group
+// sums (published by a barrier); returns the root to every thread.
+__device__ __forceinline__ float upper_tree(int64_t m1, float (&lvl)[2][2048]) {
+    const int lane = lane_id(), wave = threadIdx.x / kWave, nw = kObFinalizeThreads / kWave;
+    int cur = 0;
+    bool done = m1 <= kObTile;
+    int64_t m = (m1 + kObTile - 1) / kObTile;
+    while (!done) {
+        const int64_t g = (m + kObTile - 1) / kObTile;
+        for (int64_t i = wave; i < g; i += nw) {
+            const float s = tile_from(lvl[cur], i * kObTile, m, lane);
+            if (lane == 0) lvl[cur ^ 1][i] = s;
+        }
+        __syncthreads();
+        done = m <= kObTile;
+        cur ^= 1;
+        m = g;
+    }
+    return lvl[cur][0];
+}
+
 // The fixed 1024-tree over a chunk's m1 tile partials get(r), by one
 // kObFinalizeThreads workgroup: level 1 -> 2 straight from `get` (each wave takes
 // kFinBatch groups at once and issues all their loads -- clamped, unconditional --
@@ -239,21 +260,7 @@ __device__ __forceinline__ float chunk_tree(const Get& get, int64_t m1, float (&
         }
     }
     __syncthreads();
-    int cur = 0;
-    bool done = m <= kObTile;
-    m = g1;
-    while (!done) {
-        const int64_t g = (m + kObTile - 1) / kObTile;
-        for (int64_t i = wave; i < g; i += nw) {
-            const float s = tile_from(lvl[cur], i * kObTile, m, lane);
-            if (lane == 0) lvl[cur ^ 1][i] = s;
-        }
-        __syncthreads();
-        done = m <= kObTile;
-        cur ^= 1;
-        m = g;
-    }
-    return lvl[cur][0];
+    return upper_tree(m1, lvl);
 }
 
 __global__ __launch_bounds__(kObFinalizeThreads) void onebit_finalize_kernel(
@@ -616,8 +623,32 @@ __global__ __launch_bounds__(kObFinalizeThreads) void onebit_one_rank_kernel(con
         }
     const float pfull = wave_tree_sum(lane_tree(full));
     const float plast = rem ? wave_tree_sum(lane_tree(last)) : pfull;
-    const int64_t nfull = n / kObTile;
-    const float total2 = chunk_tree([=](int64_t r) { return r < nfull ? pfull : plast; }, m1, lvl);
+    // level 1 of the second tree without its 2^18 inputs: every group of 1024 full tiles
+    // folds to the same value; only the group holding the ragged tile (or the ragged end
+    // of the tile list) differs
+    const int64_t nfull = n / kObTile;  // full tiles; the ragged one (if any) is tile nfull
+    const int64_t g1 = (m1 + kObTile - 1) / kObTile;
+    float grp[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) grp[k][e] = pfull;
+    const float gfull = wave_tree_sum(lane_tree(grp));
+    const int64_t lastg = g1 - 1, lb = lastg * kObTile;  // the last group: tiles [lb, m1)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t r = lb + k * 256 + lane * 4 + e;
+            grp[k][e] = r < nfull ? pfull : (r < m1 ? plast : 0.0f);
+        }
+    const float glast = wave_tree_sum(lane_tree(grp));
+    float total2 = 0.0f;
+    if (m1 > 0) {
+        for (int64_t i = threadIdx.x; i < g1; i += kObFinalizeThreads) lvl[0][i] = i == lastg ? glast : gfull;
+        __syncthreads();
+        total2 = upper_tree(m1, lvl);
+    }
     if (threadIdx.x == 0) {
         OneRankOut o;
         o.scale2 = n > 0 ? total2 / (float)n : 0.0f;

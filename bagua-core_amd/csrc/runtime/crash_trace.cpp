@@ -36,10 +36,21 @@ struct Install {
     Install() {
         const char* e = std::getenv("BAGUA_SEGV_TRACE");
         if (!e || *e != '1') return;
+        // backtrace()'s first call may dlopen the unwinder and allocate, which a signal
+        // handler must not do: call it once now, so the handler's call is the cheap one
+        void* warm[4];
+        (void)backtrace(warm, 4);
+        // an alternate stack, so a stack overflow is reported too
+        static char alt[64 * 1024];
+        stack_t ss;
+        std::memset(&ss, 0, sizeof ss);
+        ss.ss_sp = alt;
+        ss.ss_size = sizeof alt;
+        (void)sigaltstack(&ss, nullptr);
         struct sigaction sa;
         std::memset(&sa, 0, sizeof sa);
         sa.sa_sigaction = on_fault;
-        sa.sa_flags = SA_SIGINFO;
+        sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
         sigemptyset(&sa.sa_mask);
         sigaction(SIGSEGV, &sa, &g_prev_segv);
         sigaction(SIGBUS, &sa, &g_prev_bus);

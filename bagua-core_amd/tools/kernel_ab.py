@@ -127,6 +127,36 @@ def workloads(dev, sp):
         return go, y
     W["one_rank_minmax_1g"] = (lambda lib: one_rank_setup(lib, False), 12 * ng)
     W["one_rank_onebit_1g"] = (lambda lib: one_rank_setup(lib, True), 8 * ng + ng // 4)
+
+    # whole comm ops at one rank through the C ABI (libbagua_core.so, a loopback communicator
+    # on this stream): in-tree build only (op_*), timed by events around the call
+    def op_setup(kind):
+        from bagua_core.communicator import loopback_communicators
+        comm = loopback_communicators(1, 0)[0]
+        cst = ctypes.c_void_p(comm.stream_ptr())
+        if kind == "ring":
+            ts = {k: ring[k].clone() for k in "twlr"}
+            raws = {k: N.bagua_tensor_t(ts[k].data_ptr(), nb, nb, BF16, 0) for k in "twlr"}
+
+            def go():
+                for k in "twlr":
+                    ts[k].copy_(ring[k])
+                torch.cuda.synchronize()
+                return lambda: N.C.bagua_decentralized_low_precision_synchronous(
+                    comm.handle, *[ctypes.byref(raws[k]) for k in "twlr"], N.COMPRESSION_MINMAX_UINT8)
+            return go, ts["l"], comm
+        y = xg.clone()
+        raw = N.bagua_tensor_t(y.data_ptr(), ng, ng, F32, 0)
+        method = N.COMPRESSION_ONEBIT if kind == "onebit" else N.COMPRESSION_MINMAX_UINT8
+
+        def go():
+            y.copy_(xg)
+            torch.cuda.synchronize()
+            return lambda: N.C.bagua_centralized_low_precision_synchronous(comm.handle, ctypes.byref(raw), 1, method)
+        return go, y, comm
+    W["op_ring_bf16_p1"] = (lambda lib: op_setup("ring"), 30 * nb)
+    W["op_onebit_1g_p1"] = (lambda lib: op_setup("onebit"), 8 * ng + ng // 4)
+    W["op_minmax_1g_p1"] = (lambda lib: op_setup("minmax"), 12 * ng)
     return W
 
 
@@ -136,13 +166,23 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--only", default="")
+    ap.add_argument("--variants", default="",
+                    help='JSON list of environment dicts: the in-tree build under each (knob sweeps), '
+                         'instead of the A/B of two builds')
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream(device=dev)
     sp = ctypes.c_void_p(st.cuda_stream)
     libs = {"B": load(N.KERNELS_PATH)}
-    if a.base:
+    envs = {"B": {}}
+    if a.variants:
+        base = libs["B"]
+        libs, envs = {}, {}
+        for i, e in enumerate(json.loads(a.variants)):
+            libs[f"v{i}"], envs[f"v{i}"] = base, {k: str(v) for k, v in e.items()}
+    elif a.base:
         libs["A"] = load(os.path.abspath(a.base))
+        envs["A"] = {}
     W = workloads(dev, sp)
     names = [n for n in W if not a.only or n in a.only.split(",")]
     res = {}
@@ -155,35 +195,49 @@ def main():
                 lib = libs[k]
                 if not hasattr(lib, "bagua_onebit_centralized_one_rank") and "onebit" in name:
                     continue
+                if name.startswith("op_") and lib is not libs.get("B", lib):
+                    continue  # whole ops run through the in-tree libbagua_core.so only
+                saved = {e: os.environ.get(e) for e in envs[k]}
+                os.environ.update(envs[k])
                 with torch.cuda.stream(st):
-                    go, out = setup(lib)
+                    made = setup(lib)
+                    go, out = made[0], made[1]
+                    tst = torch.cuda.ExternalStream(made[2].stream_ptr()) if len(made) > 2 else st
                     for i in range(a.reps + 2):
                         fn = go()  # per-launch untimed reset (in-place workloads)
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        multi = name.startswith("one_rank")  # several launches: events around the call
-                        e0.record(st)
+                        multi = name.startswith(("one_rank", "op_"))  # several launches: events around the call
+                        e0.record(tst)
                         if multi:
                             rc = fn()
-                            e1.record(st)
+                            e1.record(tst)
                         else:
-                            e1.record(st)
+                            e1.record(tst)
                             assert lib.bagua_time_next_kernel(ctypes.c_void_p(e0.cuda_event),
                                                               ctypes.c_void_p(e1.cuda_event)) == 0
                             rc = fn()
                         assert rc == 0, (name, k, rc)
-                        st.synchronize()
+                        tst.synchronize()
                         if i >= 2:
                             times[k].append(e0.elapsed_time(e1) * 1e3)
                     outs[k] = out.view(torch.uint8).clone()
                 torch.cuda.synchronize()
+                for e, v in saved.items():
+                    if v is None:
+                        os.environ.pop(e, None)
+                    else:
+                        os.environ[e] = v
         entry = {}
         for k, v in times.items():
             if v:
                 med = statistics.median(v)
                 entry[k] = {"us_median": round(med, 2), "us_min": round(min(v), 2), "gb_s": round(alg / med / 1e3, 1),
                             "frac_of_8tbs": round(alg / med / 1e3 / 8000, 4)}
-        if len(outs) == 2:
-            entry["same_bytes"] = bool(torch.equal(outs["A"], outs["B"]))
+        if len(outs) >= 2:
+            ref = outs[sorted(outs)[0]]
+            entry["same_bytes"] = all(bool(torch.equal(ref, o)) for o in outs.values())
+        if a.variants:
+            entry["env"] = envs
         entry["alg_bytes"] = alg
         res[name] = entry
         print(json.dumps({name: entry}), file=sys.stderr, flush=True)

@@ -78,6 +78,14 @@ def main():
         row.update({"quantise_piece_us": [round(v, 1) for v in q_us], "reduce_piece_us": [round(v, 1) for v in r_us],
                     "requantise_piece_us": [round(v, 1) for v in rq_us],
                     "dequantise_piece_us": [round(v, 1) for v in d_us]})
+        # algorithmic bytes per launch: piece q covers L_q elements of every chunk
+        L = [rng(q)[1] - rng(q)[0] for q in range(P)]
+        rate = lambda byts, us: round(byts / us / 1e3, 1)  # GB/s
+        row["minmax_pass_gb_s"] = rate(4 * n, row["minmax_pass_us"])              # x read once
+        row["quantise_piece_gb_s"] = [rate(5 * p * L[q], q_us[q]) for q in range(P)]  # x read, payload written
+        row["reduce_piece_gb_s"] = [rate(p * L[q], r_us[q]) for q in range(P)]        # p received payloads read
+        row["requantise_piece_gb_s"] = [rate((p + 1) * L[q], rq_us[q]) for q in range(P)]  # p read + own written
+        row["dequantise_piece_gb_s"] = [rate(5 * p * L[q], d_us[q]) for q in range(P)]  # p payloads read, x written
         row["prefix_us"] = round(row["minmax_pass_us"] + q_us[0], 1)
         row["middle_us"] = round(r_us[-1] + rq_us[0], 1)
         row["suffix_us"] = round(d_us[-1], 1)
@@ -107,6 +115,11 @@ def main():
         m_us = timed(lambda: K.bagua_onebit_reduce_requantize(0, cp, S, cs, p, None, 1, rp, S, p - 1, wp, wsb, sp))
         d_us = [timed(lambda q=q: K.bagua_onebit_decompress_range(0, cp, S, cs, p, xp, *trng(q), sp))
                 for q in range(P)]
+        TL = [trng(q)[1] - trng(q)[0] for q in range(P)]  # tiles of 1024 elements per chunk
+        out[f"onebit_p{p}_gb_s"] = {
+            "encode_piece": [round(p * t * (4096 + 128) / us / 1e3, 1) for t, us in zip(TL, e_us)],
+            "decode_piece": [round(p * t * (4096 + 128) / us / 1e3, 1) for t, us in zip(TL, d_us)],
+            "middle": round((p + 1) * sum(TL) * 128 / m_us / 1e3, 1)}
         out[f"onebit_p{p}"] = {"encode_piece_us": [round(v, 1) for v in e_us], "finalize_us": round(f_us, 1),
                                "middle_us": round(m_us, 1), "decode_piece_us": [round(v, 1) for v in d_us],
                                "codec_total_us": round(sum(e_us) + f_us + m_us + sum(d_us), 1)}

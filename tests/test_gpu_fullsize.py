@@ -1,8 +1,8 @@
 """Config 4 at BASELINE.json's full size, checked through size-independent
 properties (the oracle simulation of 8 ranks x 1 GiB would take minutes of CPU
-time): 8 virtual ranks on the loopback transport each own a 1 GiB fp32
-gradient (2^28 elements, p = 8 chunks of 2^25), run the default (pipelined,
-fused) compressed all-reduce, and then
+time): p = 2, 4 or 8 virtual ranks on the loopback transport each own a 1 GiB
+fp32 gradient (2^28 elements, p chunks of 2^28 / p), run the default
+(pipelined, fused) compressed all-reduce, and then
 
   * every rank holds the same bytes (the allgather's guarantee), and
   * each element is within the format's two-quantisation bound of the exact
@@ -22,11 +22,13 @@ from test_gpu_multirank import run_ranks
 pytestmark = pytest.mark.gpu
 
 
-def test_centralized_allreduce_1gib_p8_properties():
+@pytest.mark.parametrize("p", [2, 4, 8])
+def test_centralized_allreduce_1gib_properties(p):
+    """Config 4 at 2, 4 and 8 ranks, 1 GiB fp32 per rank (every point of the 1/2/4/8 curve)."""
     import bagua_core
     from bagua_core.communicator import loopback_communicators
     N = bagua_core._native
-    p, n = 8, 1 << 28
+    n = 1 << 28
     cs = n // p
     xs = []
     for r in range(p):
