@@ -439,7 +439,8 @@ __global__ __launch_bounds__(kBlock) void minmax_one_rank_kernel(typename T::sto
     __syncthreads();
 
     // reverse sweep: the min/max pass read the tail last, so it is re-read from the
-    // Infinity Cache first
+    // Infinity Cache first.  (Software-pipelining the next tile's loads ahead of this
+    // tile's stores measured no gain at 25 MiB or 1 GiB: profiles/r05_small_sweep2.json.)
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int64_t base = (ntiles - 1 - t) * kVecPerBlockTile;
         if (base + kVecPerBlockTile <= nvec) {

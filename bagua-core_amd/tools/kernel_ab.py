@@ -125,6 +125,30 @@ def workloads(dev, sp):
             y.copy_(xg)
             return lambda: fn(F32, y.data_ptr(), ng, 1, ws.data_ptr(), wsb, sp)
         return go, y
+    # Bagua's default 25 MiB bucket (the scheduler workload's unit): the one-rank op's two
+    # kernels, and the one-launch encode of the same bucket (what a one-launch one-rank op
+    # would cost before its larger write)
+    ns = (25 << 20) // 4
+    xs = torch.randn(ns, device=dev, generator=g) * 1e-3
+
+    def small_setup(lib, encode):
+        if encode:
+            S = lib.bagua_minmax_u8_compressed_bytes(F32, ns, 1)
+            wsb = lib.bagua_minmax_u8_workspace_bytes(ns, 1)
+            cb = torch.empty(S, dtype=torch.uint8, device=dev)
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            return (lambda: (lambda: lib.bagua_minmax_u8_compress(F32, xs.data_ptr(), ns, ns, 1, cb.data_ptr(), S,
+                                                                  ws.data_ptr(), wsb, -1, sp))), cb
+        wsb = lib.bagua_minmax_u8_workspace_bytes(ns, 1)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        y = xs.clone()
+
+        def go():
+            y.copy_(xs)
+            return lambda: lib.bagua_minmax_u8_centralized_one_rank(F32, y.data_ptr(), ns, 1, ws.data_ptr(), wsb, sp)
+        return go, y
+    W["one_rank_minmax_25m"] = (lambda lib: small_setup(lib, False), 12 * ns)
+    W["one_rank_encode_25m"] = (lambda lib: small_setup(lib, True), 9 * ns)
     W["one_rank_minmax_1g"] = (lambda lib: one_rank_setup(lib, False), 12 * ng)
     W["one_rank_onebit_1g"] = (lambda lib: one_rank_setup(lib, True), 8 * ng + ng // 4)
 

@@ -697,6 +697,10 @@ def allreduce_p1(args, n: int = 1 << 28):
     def fp32():
         N.check(N.C.bagua_centralized_full_precision_synchronous(comm.handle, ctypes.byref(raw), 1), "fp32 allreduce")
 
+    def onebit():  # the same op with the 1-bit codec (at one rank: bagua_onebit_centralized_one_rank)
+        N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
+                                                              N.COMPRESSION_ONEBIT, 0), "1-bit allreduce")
+
     def timed(fn, steps, warm):
         for _ in range(warm):
             fn()
@@ -709,6 +713,7 @@ def allreduce_p1(args, n: int = 1 << 28):
 
     t_op = timed(op, args.steps, args.warmup)
     t_f = timed(fp32, max(3, args.steps // 2), max(1, args.warmup // 2))
+    t_ob = timed(onebit, max(3, args.steps // 2), max(1, args.warmup // 2))
     # every kernel of the op, a few times (the op syncs its stream before returning)
     reps, per, names = 5, {}, []
     for _ in range(reps):
@@ -737,6 +742,7 @@ def allreduce_p1(args, n: int = 1 << 28):
            "n_ranks": 1, "ms_per_step": round(t_op * 1e3, 4), "gib_s": round(4.0 * n / t_op / GiB, 2),
            "fp32_allreduce_ms_per_step": round(t_f * 1e3, 4), "fp32_allreduce_gib_s": round(4.0 * n / t_f / GiB, 2),
            "ratio_vs_fp32": round(t_f / t_op, 3),
+           "onebit_ms_per_step": round(t_ob * 1e3, 4), "onebit_gib_s": round(4.0 * n / t_ob / GiB, 2),
            "op_kernels_us": {k: round(v, 2) for k, v in kern.items()}, "roofline": roof,
            "note": "the N > 1 lines' workload (--workload allreduce) at one rank; kernel times are the "
                    "kernels' own HIP events inside the op (bagua_time_next_kernels)"}
