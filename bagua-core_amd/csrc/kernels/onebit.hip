@@ -595,13 +595,31 @@ struct OneRankOut {
     uint32_t pad;
 };
 
+// Level 1 of the first scale's tree across the whole GPU: group g (1024 tile partials)
+// -> level1[g], one wave per group -- the same fold chunk_tree's level 1 does in one
+// workgroup, where 2^18 partials (1 GiB) took that workgroup 16 us
+__global__ __launch_bounds__(kBlock) void onebit_tree_level1_kernel(const float* __restrict__ partials, int64_t m1,
+                                                                   float* __restrict__ level1) {
+    const int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t g1 = (m1 + kObTile - 1) / kObTile;
+    if (g >= g1) return;
+    const float s = tile_from(partials, g * kObTile, m1, lane_id());
+    if (lane_id() == 0) level1[g] = s;
+}
+
 template <typename T>
-__global__ __launch_bounds__(kObFinalizeThreads) void onebit_one_rank_kernel(const float* __restrict__ partials,
+__global__ __launch_bounds__(kObFinalizeThreads) void onebit_one_rank_kernel(const float* __restrict__ level1,
                                                                             int64_t n, int average, float pf,
                                                                             OneRankOut* __restrict__ out) {
     __shared__ float lvl[2][2048];
     const int64_t m1 = (n + kObTile - 1) / kObTile;
-    const float total1 = chunk_tree([partials](int64_t r) { return partials[r]; }, m1, lvl);
+    float total1 = 0.0f;
+    if (m1 > 0) {  // the first tree from its level-1 sums (onebit_tree_level1_kernel)
+        const int64_t g1 = (m1 + kObTile - 1) / kObTile;
+        for (int64_t i = threadIdx.x; i < g1; i += kObFinalizeThreads) lvl[0][i] = level1[i];
+        __syncthreads();
+        total1 = upper_tree(m1, lvl);
+    }
     __syncthreads();  // every thread has read the first tree's root before lvl is reused
     const float scale1 = n > 0 ? total1 / (float)n : 0.0f;
     // the table kernel's p = 1 entries: segment 0 decodes to +-scale1 as stored in T
@@ -846,17 +864,23 @@ static int ob_one_rank_impl(void* tensor, int n, int average, void* ws, size_t w
     if (n < 0 || (!tensor && n > 0) || !ws || (uintptr_t)ws % 16) return BAGUA_ERR_INVALID_ARG;
     const int64_t tiles = ob_tiles(n);
     const int64_t off = onerank_partials_offset(tiles);
-    if (ws_bytes < (size_t)(off + (tiles > 0 ? tiles : 1) * (int64_t)sizeof(float))) return BAGUA_ERR_WORKSPACE;
+    const int64_t g1 = (tiles + kObTile - 1) / kObTile;
+    if (ws_bytes < (size_t)(off + ((tiles > 0 ? tiles : 1) + g1) * (int64_t)sizeof(float))) return BAGUA_ERR_WORKSPACE;
     uint8_t* seg = static_cast<uint8_t*>(ws);
     float* partials = reinterpret_cast<float*>(seg + off);
+    float* level1 = partials + (tiles > 0 ? tiles : 1);
     // 1. sign bits + |x| tile partials of the whole tensor (one chunk)
     if (tiles > 0) {
         const int rc = ob_compress_impl<T>(tensor, n, n, 1, seg, (size_t)(32 + tiles * kObTileBytes), partials,
                                            (size_t)tiles * sizeof(float), -1, s, 1, 0, tiles);
         if (rc) return rc;
     }
-    // 2. scale1, the two reduced values, scale2
-    launch(onebit_one_rank_kernel<T>, dim3(1), dim3(kObFinalizeThreads), 0, s, partials, (int64_t)n, average, 1.0f,
+    // 2. scale1 (level 1 of its tree across the GPU, the rest in one workgroup), the two
+    // reduced values, scale2
+    if (g1 > 0)
+        launch(onebit_tree_level1_kernel, dim3((unsigned)((g1 + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0,
+               s, partials, tiles, level1);
+    launch(onebit_one_rank_kernel<T>, dim3(1), dim3(kObFinalizeThreads), 0, s, level1, (int64_t)n, average, 1.0f,
            reinterpret_cast<OneRankOut*>(seg));
     // 3. the result, from the bits (store policy as the decode's, by size)
     if (tiles > 0) {
@@ -881,7 +905,8 @@ extern "C" {
 
 size_t bagua_onebit_one_rank_workspace_bytes(int num_elem) {
     const int64_t tiles = ob_tiles(num_elem < 0 ? 0 : num_elem);
-    return (size_t)(onerank_partials_offset(tiles) + (tiles > 0 ? tiles : 1) * (int64_t)sizeof(float));
+    const int64_t g1 = (tiles + kObTile - 1) / kObTile;
+    return (size_t)(onerank_partials_offset(tiles) + ((tiles > 0 ? tiles : 1) + g1) * (int64_t)sizeof(float));
 }
 
 int bagua_onebit_centralized_one_rank(int dtype, void* tensor, int num_elem, int average, void* workspace,
