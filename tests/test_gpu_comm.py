@@ -177,9 +177,11 @@ def test_op_captured_into_a_hip_graph(bc, comm, oracle_c, method):
         finally:
             assert N.C.bagua_pool_capture_end(arena) == 0
         held = N.C.bagua_pool_bytes_in_use(0) - in_use
-        # the compressed buffers stay with the graph (the MinMax op at one rank has none: it
-        # runs as the min/max pass + one table pass over the tensor, bagua_minmax_u8_centralized_one_rank)
-        assert held > 0 or code == N.COMPRESSION_MINMAX_UINT8
+        # compressed buffers would stay with the graph; the op at one rank has none (MinMax:
+        # the min/max pass + one table pass over the tensor, bagua_minmax_u8_centralized_one_rank;
+        # 1-bit: encode, scales, +-scale2 pass on the stream's workspace,
+        # bagua_onebit_centralized_one_rank)
+        assert held >= 0 and (held > 0 or comm.nranks() == 1)
         for x, w in zip(reversed(xs), reversed(want)):
             t.copy_(torch.from_numpy(x))
             torch.cuda.synchronize()
