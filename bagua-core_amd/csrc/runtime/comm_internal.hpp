@@ -88,7 +88,8 @@ struct BaguaSingleCommunicatorC {
     // that share this one's transport, rank and device but own their streams, side
     // streams and events, so consecutive buckets' ops run on different streams and
     // bucket b+1's codec prefix overlaps bucket b's exchange and tail.  The claim this
-    // rests on: RCCL (the NCCL 2.27.7 code base of ROCm 7.2's librccl) runs one
+    // rests on: RCCL (2.26.6, the librccl that PyTorch 2.10+rocm7.0 loads first and this
+    // library binds to; /opt/rocm's 2.27.7 otherwise) runs one
     // communicator's operations in the order they are issued whatever the user stream
     // -- every launch of a communicator is chained behind the previous one on the
     // communicator's internal device stream before the user stream joins it -- and the

@@ -147,8 +147,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GiB = float(1 << 30)
 SIDE_TIMEOUT_S = 120.0  # N > 1 side measurements: abort the communicator instead of hanging
 HEADLINE_TIMEOUT_S = 300.0  # N > 1 headline (pipelined op): abort, then measure the unpieced op
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_traffic.json")
-PMC_SUMMARY_ONEBIT = os.path.join(ROOT, "profiles", "r04_pmc_traffic_onebit.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")
+PMC_SUMMARY_ONEBIT = os.path.join(ROOT, "profiles", "r05_pmc_traffic_onebit.json")
 
 
 def parse():
