@@ -745,7 +745,10 @@ def allreduce_p1(args, n: int = 1 << 28):
            "onebit_ms_per_step": round(t_ob * 1e3, 4), "onebit_gib_s": round(4.0 * n / t_ob / GiB, 2),
            "op_kernels_us": {k: round(v, 2) for k, v in kern.items()}, "roofline": roof,
            "note": "the N > 1 lines' workload (--workload allreduce) at one rank; kernel times are the "
-                   "kernels' own HIP events inside the op (bagua_time_next_kernels)"}
+                   "kernels' own HIP events inside the op (bagua_time_next_kernels)",
+           "ratio_note": "at one rank RCCL's fp32 all-reduce is its single-rank reduce-copy (oneRankReduce, "
+                         "~0.19 of HBM peak): ratio_vs_fp32 here is not the multi-GPU ratio the >= 6x target "
+                         "is about"}
     del comm, x
     torch.cuda.empty_cache()
     return res
