@@ -343,6 +343,8 @@ static int mix_impl(void* t, const void* l, const void* r, const void* w, int n,
         launch(kern, dim3(grid), dim3(kBlock), 0, s, static_cast<S*>(t), static_cast<const S*>(l),
                static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13, f53, static_cast<uint2*>(ws));
     };
+    // (U = 2 and 8 vectors per tensor per batch measured slower than 4: mix 233 / 238 vs
+    // 228 us, profiles/r05_ring_mix_unroll_ab.json)
     if (contig && nts) go(ring_mix_kernel<T, kMixUnroll, true, true>);
     else if (contig) go(ring_mix_kernel<T, kMixUnroll, true, false>);
     else if (nts) go(ring_mix_kernel<T, kMixUnroll, false, true>);

@@ -139,35 +139,6 @@ __global__ __launch_bounds__(kBlock) void minmax_partials_kernel(
 }
 
 // ------------------------------------------------------------------------
-// partials fold, once per chunk (blockIdx.x = chunk): out[c] = the min / max keys of
-// chunk c's npartials partials.  The quantise pass then folds one partial per chunk
-// instead of every workgroup re-reading all of them: for a one-chunk bucket (the ring
-// op's bf16 bucket, the two-pass encode) that was 8192 workgroups x 1024 partials x 8 B
-// = 64 MB of L2 / Infinity-Cache reads at the start of every workgroup.
-// ------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void minmax_fold_partials_kernel(const uint2* __restrict__ partials,
-                                                                     int npartials, uint2* __restrict__ out) {
-    const int c = blockIdx.x;
-    uint32_t lo = 0xffffffffu, hi = 0xffffffffu;
-    for (int i = threadIdx.x; i < npartials; i += kBlock) {
-        const uint2 p = partials[(int64_t)c * npartials + i];
-        lo = min(lo, p.x);
-        hi = min(hi, p.y);
-    }
-    lo = wave_umin(lo);
-    hi = wave_umin(hi);
-    __shared__ uint32_t red[2][kWavesPerBlock];
-    const int w = threadIdx.x / kWave;
-    if (lane_id() == 0) { red[0][w] = lo; red[1][w] = hi; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-#pragma unroll
-        for (int i = 1; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
-        out[c] = make_uint2(lo, hi);
-    }
-}
-
-// ------------------------------------------------------------------------
 // pass 2: fold partials, write header, quantise
 // ------------------------------------------------------------------------
 template <typename T, bool kReverse>
@@ -607,28 +578,15 @@ static int compress_impl(const void* input, int in_num_elem, int cs, int p, uint
             launch(minmax_partials_kernel<T, false, false>, grid, dim3(kBlock), 0, s, src, (int64_t)in_num_elem,
                    (int64_t)cs, target, partials, INT64_MAX);
     }
-    if (stages & 2) {
-        const int qblocks =
-            blocks_for(e1 - e0, Vec<T>::N, nact, kSubtiles, tune_int("BAGUA_TUNE_QUANT_BLOCKS", kQuantBlocks));
-        // where every workgroup would re-read more than 16 MB of partials in all, fold them
-        // once per chunk first (into the workspace after the partials) and let the quantise
-        // fold one; BAGUA_QUANT_PREFOLD=0/1 forces either (A/B)
-        const int64_t fold_bytes = (int64_t)qblocks * nact * nblk * (int64_t)sizeof(uint2);
-        const int pf_env = tune_int("BAGUA_QUANT_PREFOLD", -1);
-        const bool room = (size_t)(nblk + 1) * (size_t)nact * sizeof(uint2) <= ws_bytes;
-        const bool prefold = room && nblk > 1 && (pf_env >= 0 ? pf_env == 1 : fold_bytes > ((int64_t)16 << 20));
-        const uint2* qpart = partials;
-        int qnp = nblk;
-        if (prefold) {
-            uint2* folded = partials + (size_t)nblk * nact;
-            launch(minmax_fold_partials_kernel, dim3(nact), dim3(kBlock), 0, s, partials, nblk, folded);
-            qpart = folded;
-            qnp = 1;
-        }
-        launch((minmax_quantize_kernel<T, true>), dim3(qblocks, nact), dim3(kBlock), 0, s,
-               static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, (int64_t)e0, (int64_t)e1, target,
-               qpart, qnp, out, chunk_offset, (int64_t)out_bytes, p);
-    }
+    // (Folding the partials once per chunk in a separate launch, so each quantise
+    // workgroup reads one partial instead of up to 1024, measured no faster in the ring
+    // op: 658.7 vs 664.1 us, profiles/r05_quant_prefold_ab.json.)
+    if (stages & 2)
+        launch((minmax_quantize_kernel<T, true>),
+               dim3(blocks_for(e1 - e0, Vec<T>::N, nact, kSubtiles, tune_int("BAGUA_TUNE_QUANT_BLOCKS", kQuantBlocks)),
+                    nact),
+               dim3(kBlock), 0, s, static_cast<const S*>(input), (int64_t)in_num_elem, (int64_t)cs, (int64_t)e0,
+               (int64_t)e1, target, partials, nblk, out, chunk_offset, (int64_t)out_bytes, p);
     return check_launch();
 }
 

@@ -6,3 +6,5 @@ for i in 1 2 3; do
   (cd ab_libs/r04 && timeout -k 10 200 python3 bench.py --workload backend --steps 20 --no-cpu-baseline > ../../gpurun_out/r05_ab_backend_r04_$i.json 2>/dev/null) || exit 1
   timeout -k 10 200 python3 bench.py --workload backend --steps 20 --no-cpu-baseline > gpurun_out/r05_ab_backend_r05_$i.json 2>/dev/null || exit 1
 done
+V2='[{}, {"BAGUA_RING_MIX_U":"2"}, {"BAGUA_RING_MIX_U":"8"}]'
+timeout -k 10 400 python3 bagua-core_amd/tools/kernel_ab.py --only mix_bf16,op_ring_bf16_p1 --rounds 3 --reps 6 --variants "$V2" > gpurun_out/r05_mixu.json 2> gpurun_out/r05_mixu.err || exit 1
