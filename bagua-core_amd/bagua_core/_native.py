@@ -109,6 +109,7 @@ KERNEL_SIGNATURES = {
     "bagua_ring_mix_minmax": (_i32, [_i32, _vp, _vp, _vp, _vp, _i32, _vp, _sz, _vp]),
     "bagua_ring_apply_minmax": (_i32, [_i32, _vp, _vp, _vp, _sz, _i32, _vp, _vp, _vp, _vp, _vp]),
     "bagua_ring_apply_minmax_range": (_i32, [_i32, _vp, _vp, _vp, _sz, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "bagua_ring_one_rank_minmax": (_i32, [_i32, _vp, _vp, _vp, _vp, _i32, _vp, _sz, _vp]),
     "bagua_onebit_compressed_bytes": (_sz, [_i32, _i32]),
     "bagua_onebit_workspace_bytes": (_sz, [_i32, _i32]),
     "bagua_onebit_compress": (_i32, [_i32, _vp, _i32, _i32, _i32, _vp, _sz, _vp, _sz, _i32, _vp]),

@@ -16,8 +16,14 @@
 //   ring_apply : the three dequantise+adds and the clone in one pass     17N
 // Every intermediate is rounded to T exactly where the reference stores it
 // (as_stored<T>), so all four tensors end bit-identical to the reference op.
+// One rank (its own left and right peer) runs two passes instead, 24N: the mix's
+// min/max only (8N read, nothing stored), then the mix recomputed, quantised and
+// dequantised in registers and applied to all four tensors (8N + 8N), no payload
+// (ring_one_rank_kernel, bagua_ring_one_rank_minmax).
 #include "codec_common.hpp"
 #include "launch_util.hpp"
+
+#include <type_traits>
 
 namespace bagua {
 
@@ -87,12 +93,19 @@ __device__ __forceinline__ float mix(float t, float l, float r, float w, float f
     return addmul<T>(t, w, f53);
 }
 
-template <typename T, int U, bool CONTIG = false, bool NTS = false>
+// STORE = false: the min/max partials of the mixed values only, t untouched (the
+// one-rank op's first pass; its second pass recomputes the mix, ring_one_rank_kernel).
+// TILES (without CONTIG): workgroups stride over whole U-vector tiles instead of
+// single vectors (the U loads of a stream 4 KiB apart instead of a grid apart).
+template <typename T, int U, bool CONTIG = false, bool NTS = false, bool STORE = true, bool TILES = false>
 __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* __restrict__ t,
                                                           const typename T::storage* __restrict__ l,
                                                           const typename T::storage* __restrict__ r,
                                                           const typename T::storage* __restrict__ w, int64_t n,
-                                                          float f13, float f53, uint2* __restrict__ partials) {
+                                                          float f13, float f53, uint2* __restrict__ partials,
+                                                          int64_t keep_from = INT64_MAX) {
+    // vectors from keep_from on load with the default policy (they stay in the Infinity
+    // Cache for the pass that re-reads them first; the rest non-temporally)
     constexpr int N = Vec<T>::N;
     uint32_t lo = min_space(T::init_max()), hi = max_space(-T::init_max());
     const int64_t nvec = n / N;
@@ -112,13 +125,15 @@ __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* _
             hi = min(hi, max_space_key(k));
         }
         // plain store: the quantise pass re-reads t next (NTS: non-temporal, A/B)
-        if constexpr (NTS) nt_store16(pack16<T>(ft), reinterpret_cast<uint4*>(t) + v);
+        if constexpr (!STORE) (void)v;
+        else if constexpr (NTS) nt_store16(pack16<T>(ft), reinterpret_cast<uint4*>(t) + v);
         else reinterpret_cast<uint4*>(t)[v] = pack16<T>(ft);
     };
     const uint4* t4 = reinterpret_cast<const uint4*>(t);
     const uint4* l4 = reinterpret_cast<const uint4*>(l);
     const uint4* r4 = reinterpret_cast<const uint4*>(r);
     const uint4* w4 = reinterpret_cast<const uint4*>(w);
+    auto ld = [&](const uint4* p, int64_t u) { return u >= keep_from ? p[u] : nt_load16(p + u); };
     // U vectors per tensor per iteration (4U x 16 B in flight per lane), all loads
     // issued before any is consumed; the last partial iteration goes one by one.
     // All four streams load non-temporally: default-policy t/w loads (or l/r) were
@@ -127,10 +142,10 @@ __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* _
         uint4 rt[U], rl[U], rr[U], rw[U];
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            rt[k] = nt_load16(t4 + v + k * kstep);
-            rl[k] = nt_load16(l4 + v + k * kstep);
-            rr[k] = nt_load16(r4 + v + k * kstep);
-            rw[k] = nt_load16(w4 + v + k * kstep);
+            rt[k] = ld(t4, v + k * kstep);
+            rl[k] = ld(l4, v + k * kstep);
+            rr[k] = ld(r4, v + k * kstep);
+            rw[k] = ld(w4, v + k * kstep);
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) body(v + k * kstep, rt[k], rl[k], rr[k], rw[k]);
@@ -143,21 +158,31 @@ __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* _
         int64_t base = lo;
         for (; base + tile <= hi; base += tile) batch(base + threadIdx.x, kBlock);
         for (int64_t u = base + threadIdx.x; u < hi; u += kBlock)
-            body(u, nt_load16(t4 + u), nt_load16(l4 + u), nt_load16(r4 + u), nt_load16(w4 + u));
+            body(u, ld(t4, u), ld(l4, u), ld(r4, u), ld(w4, u));
+    } else if constexpr (TILES) {
+        const int64_t tile = (int64_t)U * kBlock;
+        for (int64_t base = (int64_t)blockIdx.x * tile; base < nvec; base += (int64_t)gridDim.x * tile) {
+            if (base + tile <= nvec) {
+                batch(base + threadIdx.x, kBlock);
+            } else {
+                for (int64_t u = base + threadIdx.x; u < nvec; u += kBlock)
+                    body(u, ld(t4, u), ld(l4, u), ld(r4, u), ld(w4, u));
+            }
+        }
     } else {
         for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nvec; v += stride * U) {
             if (v + (U - 1) * stride < nvec) {
                 batch(v, stride);
             } else {
                 for (int64_t u = v; u < nvec; u += stride)
-                    body(u, nt_load16(t4 + u), nt_load16(l4 + u), nt_load16(r4 + u), nt_load16(w4 + u));
+                    body(u, ld(t4, u), ld(l4, u), ld(r4, u), ld(w4, u));
             }
         }
     }
     if (blockIdx.x == 0 && threadIdx.x < n - nvec * N) {  // ragged tail
         const int64_t j = nvec * N + threadIdx.x;
         const float x = mix<T>(T::to_f(t[j]), T::to_f(l[j]), T::to_f(r[j]), T::to_f(w[j]), f13, f53);
-        t[j] = T::from_f(x);
+        if constexpr (STORE) t[j] = T::from_f(x);
         const int32_t k = f2key(x);
         lo = min(lo, min_space_key(k));
         hi = min(hi, max_space_key(k));
@@ -312,6 +337,159 @@ __global__ __launch_bounds__(kBlock) void ring_apply_kernel(const uint8_t* __res
     }
 }
 
+// One rank (p = 1) is its own left and right peer: what it receives from both is its
+// own compressed bytes, so :126-151 become, per element, with d = dq(q(t_mixed)) under
+// the bucket's one header (n_chunks = 1),
+//   L += d;  R += d;  t = d + W;  W = t.
+// This pass folds the mix pass's min/max partials into that header (as the quantise
+// pass does), quantises and dequantises each mixed element in registers, and writes the
+// four tensors: the payload is neither written nor read back (16N bytes for bf16
+// instead of the quantise pass's 3N and the apply pass's 17N).  Every expression is the
+// one those two passes evaluate (the quantise pass's quant_pack4 / quant, the apply
+// pass's as_stored dequantisation table under the header as stored in T), so the four
+// tensors are bit-identical to the two-pass sequence (test_ring_one_rank_matches_sequence).
+// CONTIG: contiguous ranges of U-vector batches per workgroup (otherwise grid-strided).
+// MIX: t, l, r, w are the op's inputs (the first pass only folded the mixed values'
+// min/max, ring_mix_kernel<STORE = false>) and the mix is recomputed here, the same
+// three rounded addmuls, instead of being stored by the first pass and read back (2N
+// + 2N bytes); otherwise t holds the mixed values.
+template <typename T, int U, bool CONTIG, bool MIX>
+__global__ __launch_bounds__(kBlock) void ring_one_rank_kernel(typename T::storage* __restrict__ t,
+                                                               typename T::storage* __restrict__ w,
+                                                               typename T::storage* __restrict__ l,
+                                                               typename T::storage* __restrict__ r, int64_t n,
+                                                               const uint2* __restrict__ partials, int npartials,
+                                                               float f13, float f53) {
+    constexpr int N = Vec<T>::N;
+    static_assert(N % 4 == 0, "quant_pack4 packs four elements");
+    __shared__ float tab[256];
+    __shared__ uint32_t red[2][kWavesPerBlock];
+    const int64_t nvec = n / N;
+    uint4* t4 = reinterpret_cast<uint4*>(t);
+    uint4* w4 = reinterpret_cast<uint4*>(w);
+    uint4* l4 = reinterpret_cast<uint4*>(l);
+    uint4* r4 = reinterpret_cast<uint4*>(r);
+    QParams q;
+    auto body = [&](int64_t v, const uint4& rt, const uint4& rw, const uint4& rl, const uint4& rr) {
+        float ft[N], fw[N], fl[N], fr[N];
+        unpack16<T>(rt, ft);
+        unpack16<T>(rw, fw);
+        unpack16<T>(rl, fl);
+        unpack16<T>(rr, fr);
+        if constexpr (MIX) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) ft[i] = mix<T>(ft[i], fl[i], fr[i], fw[i], f13, f53);
+        }
+#pragma unroll
+        for (int i = 0; i < N; i += 4) {
+            const uint32_t b = quant_pack4(ft[i], ft[i + 1], ft[i + 2], ft[i + 3], q);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float d = tab[(b >> (8 * e)) & 0xff];
+                fl[i + e] = fl[i + e] + d;   // L += dq(from_left)
+                fr[i + e] = fr[i + e] + d;   // R += dq(from_right)
+                ft[i + e] = d + fw[i + e];   // t = dq(mine) + W
+            }
+        }
+        const uint4 ot = pack16<T>(ft);
+        nt_store16(pack16<T>(fl), l4 + v);
+        nt_store16(pack16<T>(fr), r4 + v);
+        nt_store16(ot, t4 + v);
+        nt_store16(ot, w4 + v);  // W = t (clone)
+    };
+    struct Regs {
+        uint4 rt[U], rw[U], rl[U], rr[U];
+    };
+    auto load_batch = [&](int64_t v, int64_t kstep, Regs& g) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int64_t u = v + k * kstep;
+            g.rt[k] = nt_load16(t4 + u);
+            g.rw[k] = nt_load16(w4 + u);
+            g.rl[k] = nt_load16(l4 + u);
+            g.rr[k] = nt_load16(r4 + u);
+        }
+    };
+    auto use_batch = [&](int64_t v, int64_t kstep, const Regs& g) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) body(v + k * kstep, g.rt[k], g.rw[k], g.rl[k], g.rr[k]);
+    };
+    auto one = [&](int64_t u) { body(u, nt_load16(t4 + u), nt_load16(w4 + u), nt_load16(l4 + u), nt_load16(r4 + u)); };
+    // the header from the mix pass's partials (minmax_quantize_kernel's fold) and the
+    // dequantisation table of the header as the apply pass reads it back (T values);
+    // run after the first batch's loads are out
+    auto prologue = [&]() {
+        uint32_t lo = 0xffffffffu, hi = 0xffffffffu;
+        for (int i = threadIdx.x; i < npartials; i += kBlock) {
+            const uint2 p = partials[i];
+            lo = min(lo, p.x);
+            hi = min(hi, p.y);
+        }
+        lo = wave_umin(lo);
+        hi = wave_umin(hi);
+        const int wv = threadIdx.x / kWave;
+        if (lane_id() == 0) { red[0][wv] = lo; red[1][wv] = hi; }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
+        const float mn = from_min_space(lo), mx = from_max_space(hi);
+        q = make_qparams(mn, mx);
+        const QParams qh = make_qparams(T::to_f(T::from_f(mn)), T::to_f(T::from_f(mx)));
+        static_assert(kBlock == 256, "one table entry per thread");
+        tab[threadIdx.x] = as_stored<T>(dequant(threadIdx.x, qh));
+        __syncthreads();
+    };
+    const int64_t tile = (int64_t)U * kBlock;
+    if constexpr (CONTIG) {
+        // MIX: backwards (the first pass read the tail last; it is in the Infinity Cache)
+        const int64_t bidx = MIX ? (int64_t)gridDim.x - 1 - blockIdx.x : (int64_t)blockIdx.x;
+        const int64_t per = ((nvec + gridDim.x - 1) / gridDim.x + tile - 1) / tile * tile;
+        const int64_t lo = bidx * per;
+        const int64_t hi = lo + per < nvec ? lo + per : nvec;
+        int64_t base = lo;
+        if (base + tile <= hi) {
+            Regs g;
+            load_batch(base + threadIdx.x, kBlock, g);
+            prologue();
+            use_batch(base + threadIdx.x, kBlock, g);
+            base += tile;
+        } else {
+            prologue();
+        }
+        for (; base + tile <= hi; base += tile) {
+            Regs g;
+            load_batch(base + threadIdx.x, kBlock, g);
+            use_batch(base + threadIdx.x, kBlock, g);
+        }
+        for (int64_t u = base + threadIdx.x; u < hi; u += kBlock) one(u);
+    } else {
+        // (whether a lane's first batch is whole differs between lanes here, so the
+        // prologue and its barriers come first, uniformly)
+        prologue();
+        const int64_t stride = (int64_t)gridDim.x * kBlock;
+        for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nvec; v += stride * U) {
+            if (v + (U - 1) * stride < nvec) {
+                Regs g;
+                load_batch(v, stride, g);
+                use_batch(v, stride, g);
+            } else {
+                for (int64_t u = v; u < nvec; u += stride) one(u);
+            }
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < n - nvec * N) {  // ragged tail
+        const int64_t j = nvec * N + threadIdx.x;
+        const float x = MIX ? mix<T>(T::to_f(t[j]), T::to_f(l[j]), T::to_f(r[j]), T::to_f(w[j]), f13, f53)
+                            : T::to_f(t[j]);
+        const float d = tab[quant(x, q)];
+        l[j] = T::from_f(T::to_f(l[j]) + d);
+        r[j] = T::from_f(T::to_f(r[j]) + d);
+        const typename T::storage o = T::from_f(d + T::to_f(w[j]));
+        t[j] = o;
+        w[j] = o;
+    }
+}
+
 static float round_to_t(int dtype, float f) {
     if (dtype == BAGUA_DTYPE_F16) return (float)(_Float16)f;
     if (dtype == BAGUA_DTYPE_BF16) {
@@ -338,17 +516,109 @@ static int mix_impl(void* t, const void* l, const void* r, const void* w, int n,
     // exactly that many partials.)
     const bool contig = tune_int("BAGUA_RING_MIX_CONTIG", 0) == 1;
     const bool nts = tune_int("BAGUA_RING_MIX_NTS", 0) == 1;
+    // workgroups stride over whole U-vector tiles (BAGUA_RING_MIX_TILES=0: over single
+    // vectors, the round-1..4 shape): 2^27 bf16, one box, 244 -> 219 us, the p = 1 op
+    // sequence 658 -> 631 us (profiles/r05_one_rank_ring.md)
+    const bool tiles = tune_int("BAGUA_RING_MIX_TILES", 1) == 1;
     const int grid = nblk;
     auto go = [&](auto kern) {
         launch(kern, dim3(grid), dim3(kBlock), 0, s, static_cast<S*>(t), static_cast<const S*>(l),
-               static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13, f53, static_cast<uint2*>(ws));
+               static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13, f53, static_cast<uint2*>(ws),
+               (int64_t)INT64_MAX);
     };
     // (U = 2 and 8 vectors per tensor per batch measured slower than 4: mix 233 / 238 vs
     // 228 us, profiles/r05_ring_mix_unroll_ab.json)
-    if (contig && nts) go(ring_mix_kernel<T, kMixUnroll, true, true>);
+    if (tiles && !contig && nts) go(ring_mix_kernel<T, kMixUnroll, false, true, true, true>);
+    else if (tiles && !contig) go(ring_mix_kernel<T, kMixUnroll, false, false, true, true>);
+    else if (contig && nts) go(ring_mix_kernel<T, kMixUnroll, true, true>);
     else if (contig) go(ring_mix_kernel<T, kMixUnroll, true, false>);
     else if (nts) go(ring_mix_kernel<T, kMixUnroll, false, true>);
     else go(ring_mix_kernel<T, kMixUnroll, false, false>);
+    return check_launch();
+}
+
+// ring_one_rank_kernel shapes (BAGUA_RING_ONE_RANK_CFG, A/B): vectors per tensor per
+// batch, contiguous ranges, workgroups (cap)
+struct OneRankCfg {
+    int u;
+    bool contig;
+    int max_blocks;
+};
+constexpr OneRankCfg kOneRankCfg[] = {
+    {1, true, 65536},  // 0: one 256-vector tile per workgroup (the apply pass's shape)
+    {2, true, 8192},   // 1
+    {1, true, 16384},  // 2
+    {4, false, 4096},  // 3: grid-strided
+    {2, true, 32768},  // 4
+    {2, true, 16384},  // 5
+    {4, true, 16384},  // 6
+    {4, true, 8192},   // 7
+    {8, true, 8192},   // 8
+};
+constexpr int kOneRankNumCfg = (int)(sizeof(kOneRankCfg) / sizeof(kOneRankCfg[0]));
+
+template <typename T>
+static int one_rank_impl(void* t, void* w, void* l, void* r, int n, void* ws, size_t ws_bytes, float f13, float f53,
+                         hipStream_t s) {
+    using S = typename T::storage;
+    if (!t || !w || !l || !r || n < 0) return BAGUA_ERR_INVALID_ARG;
+    if (!aligned16(t) || !aligned16(w) || !aligned16(l) || !aligned16(r)) return BAGUA_ERR_UNSUPPORTED;
+    // the mix pass (its partials count is what the fold below reads)
+    const int nblk = ws ? minmax_partials_blocks(n, Vec<T>::N, 1, ws_bytes) : 0;
+    if (nblk < 1) return BAGUA_ERR_WORKSPACE;
+    // BAGUA_RING_ONE_RANK_RECOMPUTE=0: the first pass stores the mixed t (A/B)
+    const bool recompute = tune_int("BAGUA_RING_ONE_RANK_RECOMPUTE", 1) != 0;
+    if (recompute) {
+        // BAGUA_RING_ONE_RANK_KEEP_MIB (A/B, default 0): the last MiB of the four inputs,
+        // read last here, load with the default policy to stay in the 256 MiB Infinity
+        // Cache for the second pass, which sweeps backwards and reads them first
+        const int64_t keep = (int64_t)tune_int("BAGUA_RING_ONE_RANK_KEEP_MIB", 0) << 20;
+        const int64_t nvec = (int64_t)n / Vec<T>::N;
+        int64_t keep_from = nvec - (keep > 0 ? keep / 4 / 16 : 0);
+        if (keep <= 0) keep_from = INT64_MAX;
+        else if (keep_from < 0) keep_from = 0;
+        auto go1 = [&](auto kern) {
+            launch(kern, dim3(nblk), dim3(kBlock), 0, s, static_cast<S*>(t), static_cast<const S*>(l),
+                   static_cast<const S*>(r), static_cast<const S*>(w), (int64_t)n, f13, f53, static_cast<uint2*>(ws),
+                   keep_from);
+        };
+        // first-pass shapes (BAGUA_RING_ONE_RANK_MIX_CFG, A/B; 2^27 bf16, one box, rocprof
+        // kernel trace, profiles/r05_one_rank_ring.md): 0 vector-strided U = 4, 208 us;
+        // 1 tile-strided U = 4, 184 us (default); 2 tile-strided U = 8, 190 us; 3
+        // contiguous ranges, 206 us; 4 tile-strided U = 2, 188 us
+        switch (tune_int("BAGUA_RING_ONE_RANK_MIX_CFG", 1)) {
+            case 0: go1(ring_mix_kernel<T, kMixUnroll, false, false, false>); break;
+            case 2: go1(ring_mix_kernel<T, 8, false, false, false, true>); break;
+            case 3: go1(ring_mix_kernel<T, 4, true, false, false>); break;
+            case 4: go1(ring_mix_kernel<T, 2, false, false, false, true>); break;
+            default: go1(ring_mix_kernel<T, 4, false, false, false, true>); break;
+        }
+        const int rc = check_launch();
+        if (rc != BAGUA_OK) return rc;
+    } else {
+        const int rc = mix_impl<T>(t, l, r, w, n, ws, ws_bytes, f13, f53, s);
+        if (rc != BAGUA_OK) return rc;
+    }
+    int ci = tune_int("BAGUA_RING_ONE_RANK_CFG", 0);
+    if (ci < 0 || ci >= kOneRankNumCfg) ci = 0;
+    const OneRankCfg& c = kOneRankCfg[ci];
+    int64_t blocks = ((int64_t)n / Vec<T>::N + (int64_t)c.u * kBlock - 1) / ((int64_t)c.u * kBlock);
+    if (blocks > c.max_blocks) blocks = c.max_blocks;
+    if (blocks < 1) blocks = 1;
+    auto go = [&](auto kern) {
+        launch(kern, dim3((unsigned)blocks), dim3(kBlock), 0, s, static_cast<S*>(t), static_cast<S*>(w),
+               static_cast<S*>(l), static_cast<S*>(r), (int64_t)n, static_cast<const uint2*>(ws), nblk, f13, f53);
+    };
+    auto pick = [&](auto mixc) {
+        constexpr bool M = decltype(mixc)::value;
+        if (!c.contig) go(ring_one_rank_kernel<T, 4, false, M>);
+        else if (c.u == 2) go(ring_one_rank_kernel<T, 2, true, M>);
+        else if (c.u == 4) go(ring_one_rank_kernel<T, 4, true, M>);
+        else if (c.u == 8) go(ring_one_rank_kernel<T, 8, true, M>);
+        else go(ring_one_rank_kernel<T, 1, true, M>);
+    };
+    if (recompute) pick(std::true_type{});
+    else pick(std::false_type{});
     return check_launch();
 }
 
@@ -424,6 +694,22 @@ int bagua_ring_mix_minmax(int dtype, void* tensor, const void* left, const void*
             return mix_impl<F16>(tensor, left, right, weight, num_elem, workspace, workspace_bytes, f13, f53, s);
         case BAGUA_DTYPE_BF16:
             return mix_impl<BF16>(tensor, left, right, weight, num_elem, workspace, workspace_bytes, f13, f53, s);
+    }
+    return BAGUA_ERR_UNSUPPORTED;
+}
+
+int bagua_ring_one_rank_minmax(int dtype, void* tensor, void* weight, void* left, void* right, int num_elem,
+                               void* workspace, size_t workspace_bytes, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const float f13 = round_to_t(dtype, (float)(1.0 / 3.0)), f53 = round_to_t(dtype, (float)(-5.0 / 3.0));
+    switch (dtype) {
+        case BAGUA_DTYPE_F32:
+            return one_rank_impl<F32>(tensor, weight, left, right, num_elem, workspace, workspace_bytes, f13, f53, s);
+        case BAGUA_DTYPE_F16:
+            return one_rank_impl<F16>(tensor, weight, left, right, num_elem, workspace, workspace_bytes, f13, f53, s);
+        case BAGUA_DTYPE_BF16:
+            return one_rank_impl<BF16>(tensor, weight, left, right, num_elem, workspace, workspace_bytes, f13, f53,
+                                       s);
     }
     return BAGUA_ERR_UNSUPPORTED;
 }

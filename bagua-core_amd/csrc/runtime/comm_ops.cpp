@@ -891,6 +891,18 @@ static int decentralized(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, c
     if ((rc = check_schedule(c, pipelined ? kOpRingPipelined : (allow_fused ? kOpRing : kOpRingUnfused), method, t,
                              (uint64_t)n, pipelined ? sched | (multipath ? BAGUA_PIECES_MULTIPATH : 0) : 1, 1)))
         return rc;
+    if (fused && !pipelined && c->nranks == 1 && env_int("BAGUA_ONE_RANK_FUSED", 1) != 0) {
+        // one rank: both peers' payloads are its own bytes, so the op is the mix pass and
+        // one pass applying d = dq(q(mixed)) to all four tensors, no payload written
+        // (bagua_ring_one_rank_minmax); BAGUA_ONE_RANK_FUSED=0: the steps below (A/B)
+        const size_t wsb = bagua_minmax_u8_workspace_bytes(n, 1);
+        uint64_t wsp = 0;
+        if ((rc = stream_workspace(c->device_id, s, wsb, &wsp)) != BAGUA_OK) return finish(c, rc);
+        rc = bagua_ring_one_rank_minmax(t->dtype, (void*)(uintptr_t)t->ptr, (void*)(uintptr_t)weight->ptr,
+                                        (void*)(uintptr_t)left->ptr, (void*)(uintptr_t)right->ptr, n,
+                                        (void*)(uintptr_t)wsp, wsb, sp);
+        if (rc != BAGUA_ERR_UNSUPPORTED) return finish(c, rc);
+    }
     OpBuffer mine(c), lbuf(c), rbuf(c);
     TRY(mine.allocate(c->device_id, S));
     TRY(lbuf.allocate(c->device_id, S));

@@ -285,6 +285,14 @@ int bagua_ring_apply_minmax(int dtype, const uint8_t* mine, const uint8_t* from_
 int bagua_ring_apply_minmax_range(int dtype, const uint8_t* mine, const uint8_t* from_left, const uint8_t* from_right,
                                   size_t compressed_bytes, int num_elem, int elem_begin, int elem_end, void* tensor,
                                   void* weight, void* left, void* right, bagua_stream_t stream);
+/* The whole ring op at one rank (its own left and right peer, so both peers' payloads
+ * are its own bytes): the mix pass, then one pass that folds the mix's min/max
+ * partials into the header and applies L += d, R += d, tensor = d + W, W = tensor with
+ * d = dq(q(mixed)) per element, writing no payload.  Bit-identical to mix + stage 2 +
+ * bagua_ring_apply_minmax(mine, mine, mine); the same workspace as
+ * bagua_ring_mix_minmax; BAGUA_ERR_UNSUPPORTED for tensors not 16-B aligned. */
+int bagua_ring_one_rank_minmax(int dtype, void* tensor, void* weight, void* left, void* right, int num_elem,
+                               void* workspace, size_t workspace_bytes, bagua_stream_t stream);
 
 /* K:196-266 elementwise kernels, dtype-generic (f32, f16, bf16) */
 int bagua_add_inplace(int dtype, void* x, const void* y, int n, bagua_stream_t stream);
