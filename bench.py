@@ -714,6 +714,18 @@ def allreduce_p1(args, n: int = 1 << 28):
     t_op = timed(op, args.steps, args.warmup)
     t_f = timed(fp32, max(3, args.steps // 2), max(1, args.warmup // 2))
     t_ob = timed(onebit, max(3, args.steps // 2), max(1, args.warmup // 2))
+    # config 5 at one rank: 2^27 bf16, the decentralized ring op
+    # (decentralized_low_precision_synchronous.rs:42-152; at one rank its own left and right
+    # peer: bagua_ring_one_rank_minmax, two passes)
+    nb = 1 << 27
+    ring = [(torch.randn(nb, device=dev, generator=g) * 1e-3).to(torch.bfloat16) for _ in range(4)]
+    rraws = [BaguaTensorPy(b, k).raw() for b, k in zip(ring, "twlr")]
+
+    def ring_op():
+        N.check(N.C.bagua_decentralized_low_precision_synchronous(comm.handle, *[ctypes.byref(r) for r in rraws],
+                                                                  N.COMPRESSION_MINMAX_UINT8), "ring op")
+    t_ring = timed(ring_op, max(3, args.steps // 2), max(1, args.warmup // 2))
+    del ring, rraws
     # every kernel of the op, a few times (the op syncs its stream before returning)
     reps, per, names = 5, {}, []
     for _ in range(reps):
@@ -743,6 +755,8 @@ def allreduce_p1(args, n: int = 1 << 28):
            "fp32_allreduce_ms_per_step": round(t_f * 1e3, 4), "fp32_allreduce_gib_s": round(4.0 * n / t_f / GiB, 2),
            "ratio_vs_fp32": round(t_f / t_op, 3),
            "onebit_ms_per_step": round(t_ob * 1e3, 4), "onebit_gib_s": round(4.0 * n / t_ob / GiB, 2),
+           "ring_bf16_config5_ms_per_step": round(t_ring * 1e3, 4),
+           "ring_bf16_config5_gib_s": round(2.0 * nb / t_ring / GiB, 2),
            "op_kernels_us": {k: round(v, 2) for k, v in kern.items()}, "roofline": roof,
            "note": "the N > 1 lines' workload (--workload allreduce) at one rank; kernel times are the "
                    "kernels' own HIP events inside the op (bagua_time_next_kernels)",

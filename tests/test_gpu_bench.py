@@ -106,3 +106,6 @@ def test_default_line_carries_config4_point(default_line, allreduce_line):
     assert r and r["kernel"] in {k.split(":", 1)[1] for k in ks} and 0 < r["frac"] < 1.2
     ref = allreduce_line["ms_per_step"]
     assert abs(a["ms_per_step"] - ref) <= 0.05 * ref, (a["ms_per_step"], ref)
+    # and config 5 (2^27 bf16 ring op) at one rank
+    assert a["ring_bf16_config5_ms_per_step"] > 0
+    assert abs(a["ring_bf16_config5_gib_s"] * a["ring_bf16_config5_ms_per_step"] * 1e-3 - 0.25) < 0.01
