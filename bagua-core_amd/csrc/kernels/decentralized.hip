@@ -564,10 +564,15 @@ static int one_rank_impl(void* t, void* w, void* l, void* r, int n, void* ws, si
     if (!t || !w || !l || !r || n < 0) return BAGUA_ERR_INVALID_ARG;
     if (!aligned16(t) || !aligned16(w) || !aligned16(l) || !aligned16(r)) return BAGUA_ERR_UNSUPPORTED;
     // the mix pass (its partials count is what the fold below reads)
-    const int nblk = ws ? minmax_partials_blocks(n, Vec<T>::N, 1, ws_bytes) : 0;
+    int nblk = ws ? minmax_partials_blocks(n, Vec<T>::N, 1, ws_bytes) : 0;
     if (nblk < 1) return BAGUA_ERR_WORKSPACE;
     // BAGUA_RING_ONE_RANK_RECOMPUTE=0: the first pass stores the mixed t (A/B)
     const bool recompute = tune_int("BAGUA_RING_ONE_RANK_RECOMPUTE", 1) != 0;
+    if (recompute) {  // first-pass grid (A/B; both passes here, so any count the workspace holds)
+        const int64_t want = tune_int("BAGUA_RING_ONE_RANK_MIX_BLOCKS", 0);
+        const int64_t cap = (int64_t)(ws_bytes / sizeof(uint2));
+        if (want > 0) nblk = (int)(want < cap ? want : cap);
+    }
     if (recompute) {
         // BAGUA_RING_ONE_RANK_KEEP_MIB (A/B, default 0): the last MiB of the four inputs,
         // read last here, load with the default policy to stay in the 256 MiB Infinity
