@@ -527,7 +527,8 @@ static int mix_impl(void* t, const void* l, const void* r, const void* w, int n,
                (int64_t)INT64_MAX);
     };
     // (U = 2 and 8 vectors per tensor per batch measured slower than 4: mix 233 / 238 vs
-    // 228 us, profiles/r05_ring_mix_unroll_ab.json)
+    // 228 us, profiles/r05_ring_mix_unroll_ab.json; tile-strided 228 / 222 vs 221 us,
+    // r05_ring_mix_tile_u_trace.csv)
     if (tiles && !contig && nts) go(ring_mix_kernel<T, kMixUnroll, false, true, true, true>);
     else if (tiles && !contig) go(ring_mix_kernel<T, kMixUnroll, false, false, true, true>);
     else if (contig && nts) go(ring_mix_kernel<T, kMixUnroll, true, true>);
