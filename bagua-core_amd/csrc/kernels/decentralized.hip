@@ -518,7 +518,7 @@ static int mix_impl(void* t, const void* l, const void* r, const void* w, int n,
     const bool nts = tune_int("BAGUA_RING_MIX_NTS", 0) == 1;
     // workgroups stride over whole U-vector tiles (BAGUA_RING_MIX_TILES=0: over single
     // vectors, the round-1..4 shape): 2^27 bf16, one box, 244 -> 219 us, the p = 1 op
-    // sequence 658 -> 631 us (profiles/r05_one_rank_ring.md)
+    // sequence 658 -> 631 us (profiles/r05_one_rank_ring_shapes_trace.csv)
     const bool tiles = tune_int("BAGUA_RING_MIX_TILES", 1) == 1;
     const int grid = nblk;
     auto go = [&](auto kern) {
@@ -569,7 +569,10 @@ static int one_rank_impl(void* t, void* w, void* l, void* r, int n, void* ws, si
     if (nblk < 1) return BAGUA_ERR_WORKSPACE;
     // BAGUA_RING_ONE_RANK_RECOMPUTE=0: the first pass stores the mixed t (A/B)
     const bool recompute = tune_int("BAGUA_RING_ONE_RANK_RECOMPUTE", 1) != 0;
-    if (recompute) {  // first-pass grid (A/B; both passes here, so any count the workspace holds)
+    // first-pass grid (A/B; both passes are here, so any count the workspace holds): 512 /
+    // 768 / 2048 workgroups measured against the default 1024, within noise except 2048,
+    // whose 2048 partials every second-pass workgroup folds (pass 2 352 -> 382 us)
+    if (recompute) {
         const int64_t want = tune_int("BAGUA_RING_ONE_RANK_MIX_BLOCKS", 0);
         const int64_t cap = (int64_t)(ws_bytes / sizeof(uint2));
         if (want > 0) nblk = (int)(want < cap ? want : cap);
@@ -589,7 +592,7 @@ static int one_rank_impl(void* t, void* w, void* l, void* r, int n, void* ws, si
                    keep_from);
         };
         // first-pass shapes (BAGUA_RING_ONE_RANK_MIX_CFG, A/B; 2^27 bf16, one box, rocprof
-        // kernel trace, profiles/r05_one_rank_ring.md): 0 vector-strided U = 4, 208 us;
+        // kernel trace, profiles/r05_one_rank_ring_shapes_trace.csv): 0 vector-strided U = 4, 208 us;
         // 1 tile-strided U = 4, 184 us (default); 2 tile-strided U = 8, 190 us; 3
         // contiguous ranges, 206 us; 4 tile-strided U = 2, 188 us
         switch (tune_int("BAGUA_RING_ONE_RANK_MIX_CFG", 1)) {
