@@ -518,7 +518,7 @@ static int mix_impl(void* t, const void* l, const void* r, const void* w, int n,
     const bool nts = tune_int("BAGUA_RING_MIX_NTS", 0) == 1;
     // workgroups stride over whole U-vector tiles (BAGUA_RING_MIX_TILES=0: over single
     // vectors, the round-1..4 shape): 2^27 bf16, one box, 244 -> 219 us, the p = 1 op
-    // sequence 658 -> 631 us (profiles/r05_one_rank_ring_shapes_trace.csv)
+    // sequence 658 -> 631 us (profiles/r05_one_rank_ring_mix_tiles_trace.csv)
     const bool tiles = tune_int("BAGUA_RING_MIX_TILES", 1) == 1;
     const int grid = nblk;
     auto go = [&](auto kern) {
