@@ -198,6 +198,11 @@ class PhaseClock:
     def lap(self, name: str) -> None:
         now = time.perf_counter()
         self.s[name] = self.s.get(name, 0.0) + (now - self.t)
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1 and os.environ.get("RANK", "0") == "0":
+            # progress on stderr (stdout carries only the JSON line): a long N > 1 run is
+            # visibly alive phase by phase
+            print(f"bench.py: phase {name} {now - self.t:.1f} s (process {now - _PROCESS_T0:.1f} s)",
+                  file=sys.stderr, flush=True)
         self.t = now
 
     def report(self) -> dict:
@@ -975,6 +980,9 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             wl = SchedulerWorkload(comm, world, rank, local_rank, nbk, mib)
             sched["buckets"], sched["bucket_mib"] = nbk, mib
             for ln in (wl.backend.lanes(), 1):
+                if wl.comm is not comm:  # a timed-out side line rebuilt the communicator
+                    wl.close()
+                    wl = SchedulerWorkload(comm, world, rank, local_rank, nbk, mib)
                 wl.backend.set_lanes(ln)
                 t_sc = side(f"scheduler_lanes{ln}", wl.iteration)
                 sched[f"lanes_{ln}"] = {"ms_per_step": round(t_sc * 1e3, 4),
@@ -1101,7 +1109,7 @@ class SchedulerWorkload:
     def __init__(self, comm, world: int, rank: int, local_rank: int, buckets: int, bucket_mib: int):
         import bagua_core
         dev = torch.device("cuda", local_rank)
-        self.world, self.nb = world, buckets
+        self.comm, self.world, self.nb = comm, world, buckets
         per = (bucket_mib << 20) // 4
         per -= per % (4 * 32 * world)
         self.per = per
