@@ -23,6 +23,8 @@
 #include "codec_common.hpp"
 #include "launch_util.hpp"
 
+#include <type_traits>
+
 namespace bagua {
 
 constexpr int kVecPerBlockTile = kBlock * kSubtiles;  // 1024 x 16-B vectors = 16 KiB in flight per block
@@ -381,6 +383,31 @@ __device__ __forceinline__ float one_rank_reduce(float c0) {
     else return s * 1.0f;  // mean over p = 1: the exact reciprocal (reduce.hip avg_finish)
 }
 
+// The op's parameters from the folded min/max keys: Q1 (the first quantisation) and the
+// table entry for byte b (the T bits of the op's final value for b1 = b).
+template <typename T, int AV>
+__device__ __forceinline__ uint32_t one_rank_entry(uint32_t lo, uint32_t hi, uint32_t b, QParams* q1_out) {
+    const float mn1 = from_min_space(lo), mx1 = from_max_space(hi);
+    const QParams q1 = make_qparams(mn1, mx1);
+    const bool regular = __builtin_isfinite(mn1) && __builtin_isfinite(mx1) && __builtin_isfinite(q1.scale) &&
+                         q1.scale > 0.0f;
+    auto y_of = [&](uint32_t c) { return as_stored<T>(one_rank_reduce<T, AV>(as_stored<T>(dequant(c, q1)))); };
+    float mn2 = T::init_max(), mx2 = -T::init_max();
+    if (regular) {
+        mn2 = y_of(quant(mn1, q1));
+        mx2 = y_of(quant(mx1, q1));
+    } else if (!(mn1 <= mx1)) {
+        // every element NaN (the header holds the init values): one byte value for all of
+        // them, so one y value -- the min and max of y unless it is NaN itself (the f16
+        // init header has a finite, negative scale: y = -inf there)
+        const float ys = y_of(quant(__int_as_float(0x7fc00000), q1));
+        if (!__builtin_isnan(ys)) mn2 = mx2 = ys;
+    }
+    const QParams q2 = make_qparams(mn2, mx2);
+    *q1_out = q1;
+    return stored_bits<T>(dequant(quant(y_of(b), q2), q2));
+}
+
 template <typename T, int AV>
 __global__ __launch_bounds__(kBlock) void minmax_one_rank_kernel(typename T::storage* __restrict__ x, int64_t n,
                                                                  const uint2* __restrict__ partials, int npartials) {
@@ -402,6 +429,7 @@ __global__ __launch_bounds__(kBlock) void minmax_one_rank_kernel(typename T::sto
 #pragma unroll
         for (int k = 0; k < kSubtiles; ++k) pre[k] = nt_load16(&v[base_first + k * kBlock + threadIdx.x]);
     }
+    __shared__ uint32_t lut[256];  // b1 -> the T bits of the op's final value
     uint32_t lo = 0xffffffffu, hi = 0xffffffffu;
     for (int i = threadIdx.x; i < npartials; i += kBlock) {
         const uint2 p = partials[i];
@@ -411,31 +439,14 @@ __global__ __launch_bounds__(kBlock) void minmax_one_rank_kernel(typename T::sto
     lo = wave_umin(lo);
     hi = wave_umin(hi);
     __shared__ uint32_t red[2][kWavesPerBlock];
-    __shared__ uint32_t lut[256];  // b1 -> the T bits of the op's final value
     const int w = threadIdx.x / kWave;
     if (lane_id() == 0) { red[0][w] = lo; red[1][w] = hi; }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
-    const float mn1 = from_min_space(lo), mx1 = from_max_space(hi);
-    const QParams q1 = make_qparams(mn1, mx1);
-    const bool regular = __builtin_isfinite(mn1) && __builtin_isfinite(mx1) && __builtin_isfinite(q1.scale) &&
-                         q1.scale > 0.0f;
-    auto y_of = [&](uint32_t b) { return as_stored<T>(one_rank_reduce<T, AV>(as_stored<T>(dequant(b, q1)))); };
-    float mn2 = T::init_max(), mx2 = -T::init_max();
-    if (regular) {
-        mn2 = y_of(quant(mn1, q1));
-        mx2 = y_of(quant(mx1, q1));
-    } else if (!(mn1 <= mx1)) {
-        // every element NaN (the header holds the init values): one byte value for all of
-        // them, so one y value -- the min and max of y unless it is NaN itself (the f16
-        // init header has a finite, negative scale: y = -inf there)
-        const float ys = y_of(quant(__int_as_float(0x7fc00000), q1));
-        if (!__builtin_isnan(ys)) mn2 = mx2 = ys;
-    }
-    const QParams q2 = make_qparams(mn2, mx2);
+    QParams q1;
     static_assert(kBlock == 256, "one table entry per thread");
-    lut[threadIdx.x] = stored_bits<T>(dequant(quant(y_of(threadIdx.x), q2), q2));
+    lut[threadIdx.x] = one_rank_entry<T, AV>(lo, hi, threadIdx.x, &q1);
     __syncthreads();
 
     // reverse sweep: the min/max pass read the tail last, so it is re-read from the
@@ -764,12 +775,20 @@ static int one_rank_impl(void* tensor, int num_elem, int average, void* ws, size
                static_cast<const S*>(tensor), (int64_t)num_elem, (int64_t)num_elem, -1, partials, INT64_MAX);
     const dim3 grid(
         blocks_for(num_elem, Vec<T>::N, 1, kSubtiles, tune_int("BAGUA_TUNE_ONE_RANK_BLOCKS", kOneRankBlocks)), 1);
-    if (average)
-        launch(minmax_one_rank_kernel<T, 1>, grid, dim3(kBlock), 0, s, static_cast<S*>(tensor), (int64_t)num_elem,
+    // (folding the partials and building the table once in a one-workgroup kernel, the
+    // table pass loading them, measured no faster: 25 MiB 14.9 vs 14.7 us, 1 GiB 326 vs
+    // 321 us, profiles/r05_one_rank_header_ab.json -- the per-workgroup prologue is hidden
+    // behind the first tile's loads)
+    // (default-policy stores of the result instead of non-temporal ones: 25 MiB op 23.7 ->
+    // 24.9 us, 1 GiB 512 -> 528 us, the 32 x 25 MiB scheduler line 1,496 / 1,554 -> 1,417 /
+    // 1,436 GiB/s, profiles/r05_one_rank_nts_ab.json)
+    auto go = [&](auto av) {
+        constexpr int AV = decltype(av)::value;
+        launch(minmax_one_rank_kernel<T, AV>, grid, dim3(kBlock), 0, s, static_cast<S*>(tensor), (int64_t)num_elem,
                static_cast<const uint2*>(partials), nblk);
-    else
-        launch(minmax_one_rank_kernel<T, 0>, grid, dim3(kBlock), 0, s, static_cast<S*>(tensor), (int64_t)num_elem,
-               static_cast<const uint2*>(partials), nblk);
+    };
+    if (average) go(std::integral_constant<int, 1>{});
+    else go(std::integral_constant<int, 0>{});
     return check_launch();
 }
 
