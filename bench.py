@@ -846,12 +846,16 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         nonlocal comm
         expired = []
 
+        # test hook (BAGUA_BENCH_FAIL_SIDE=<side line>): that line's limit is 0 s, so its
+        # communicator is aborted at once and the recovery below runs
+        limit = 0.0 if os.environ.get("BAGUA_BENCH_FAIL_SIDE") == name else SIDE_TIMEOUT_S
+
         def expire():
             expired.append(True)
-            side_errors[name] = f"timed out after {SIDE_TIMEOUT_S} s; communicator aborted and rebuilt"
+            side_errors[name] = f"timed out after {limit} s; communicator aborted and rebuilt"
             comm.abort()
 
-        timer = threading.Timer(SIDE_TIMEOUT_S, expire)
+        timer = threading.Timer(limit, expire)
         timer.daemon = True
         timer.start()
         res = float("nan")

@@ -159,6 +159,29 @@ def test_hierarchical(tmp_path, oracle_c):
         assert np.array_equal(o["t"], want[r // per_node].view(np.uint8)), r
 
 
+def test_bench_side_line_timeout_recovers(tmp_path):
+    """A side line past its limit (BAGUA_BENCH_FAIL_SIDE: the scheduler's lanes run, limit 0 s)
+    aborts the communicator; every rank rebuilds it, the scheduler workload is rebuilt on
+    the new one, and the remaining side lines (one lane, 1-bit, config 5) still measure."""
+    import json
+    env = dict(os.environ)
+    env.update({"BAGUA_BENCH_SHARED_GPU": "1", "NCCL_IB_DISABLE": "1", "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+                "BAGUA_BENCH_FAIL_SIDE": "scheduler_lanes3"})
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--elements", str(1 << 22), "--cpu-seconds", "1"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["value"] > 0 and "headline_fallback" not in d, d
+    assert set(d["side_errors"]) == {"scheduler_lanes3"}, d["side_errors"]
+    sc = d["scheduler_buckets"]
+    assert sc["lanes_1"]["ms_per_step"] > 0, sc
+    assert d["onebit_allreduce"]["ms_per_step"] > 0 and d["decentralized_bf16"]["ms_per_step"] > 0
+
+
 @pytest.mark.parametrize("world,fail_headline,launcher", [(2, False, "self"), (8, False, "self"),
                                                           (2, True, "torchrun")])
 def test_bench_line_multirank(tmp_path, world, fail_headline, launcher):
