@@ -264,6 +264,37 @@ def test_decentralized_pipelined_multirank(bc, oracle_c, p, dtype, n, pieces, ta
             assert np.array_equal(host(dts[k][r], dtype).view(np.uint8), wk[r].view(np.uint8)), f"{k} rank {r}"
 
 
+@pytest.mark.parametrize("mix_env", [{"BAGUA_RING_MIX_TILES": "0"}, {"BAGUA_RING_MIX_NTS": "1"},
+                                     {"BAGUA_RING_MIX_TILES": "0", "BAGUA_RING_MIX_CONTIG": "1"}])
+@pytest.mark.parametrize("p,dtype,n,pieces", [(2, BF16, (1 << 20) + 37, 1), (4, F32, 70001, 3)])
+def test_ring_mix_shapes_multirank(bc, oracle_c, p, dtype, n, pieces, mix_env, monkeypatch):
+    """The mix pass's other shapes (vector-strided -- the shape before round 5's tile-strided
+    default --, non-temporal stores of the mixed t, contiguous ranges) leave every tensor of
+    the ring op as the oracle's simulation has it: the min/max partials fold to the same
+    header whatever the workgroups' ranges."""
+    for k, v in mix_env.items():
+        monkeypatch.setenv(k, v)
+    from bagua_core.communicator import loopback_communicators
+    rng = np.random.default_rng(77 + p + n + pieces)
+    arrs = {k: [NP.from_f32((rng.standard_normal(n) * 1e-3).astype(np.float32), dtype) for _ in range(p)]
+            for k in "twlr"}
+    want = simulate.decentralized_low_precision(oracle_c, arrs["t"], arrs["w"], arrs["l"], arrs["r"], dtype)
+    comms = loopback_communicators(p, 0)
+    dts = {k: [dev(a, dtype) for a in arrs[k]] for k in "twlr"}
+    torch.cuda.synchronize()
+    N = bc._native
+
+    def rank(r):
+        raws = [bc.BaguaTensorPy(dts[k][r], k).raw() for k in "twlr"]
+        N.check(N.C.bagua_decentralized_low_precision_pipelined(comms[r].handle, *[ctypes.byref(x) for x in raws],
+                                                                N.COMPRESSION_MINMAX_UINT8, pieces), f"rank {r}")
+
+    run_ranks(rank, p)
+    for k, wk in zip("twlr", want):
+        for r in range(p):
+            assert np.array_equal(host(dts[k][r], dtype).view(np.uint8), wk[r].view(np.uint8)), f"{k} rank {r}"
+
+
 def test_pipelined_ops_back_to_back_fuzz(bc, oracle_c):
     """Random shapes, rank counts and piece counts, every pipelined op run twice in a row on
     the same loopback communicators (pool buffers, events and workspaces are reused across
