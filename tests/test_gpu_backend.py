@@ -412,12 +412,14 @@ def test_lanes_pipelined_op_buckets(bc, oracle_c, lanes):
     del backends
 
 
-def test_lanes_mixed_ops_multirank(bc, oracle_c):
-    """Two lanes, p = 2 on the loopback transport, buckets alternating between the 1-bit
-    centralized op and the decentralized ring op (its weight/peer tensors per bucket):
-    every bucket on every rank equals the oracle's simulation, two iterations."""
+@pytest.mark.parametrize("p,lanes", [(2, 2), (1, 3)])
+def test_lanes_mixed_ops_multirank(bc, oracle_c, p, lanes):
+    """Lanes on the loopback transport, buckets alternating between the 1-bit centralized op
+    and the decentralized ring op (its weight/peer tensors per bucket): every bucket on every
+    rank equals the oracle's simulation, two iterations.  p = 1 runs both ops' one-rank forms
+    (two passes each) on three lane streams."""
     from bagua_core.communicator import loopback_communicators
-    p, nb, n = 2, 4, 3 * 16384
+    nb, n = 4, 3 * 16384
     comms = loopback_communicators(p, 0)
     rng = np.random.default_rng(4711)
     host = {(r, b, k): (rng.standard_normal(n) * 1e-3).astype(np.float32) for r in range(p) for b in range(nb)
@@ -438,7 +440,7 @@ def test_lanes_mixed_ops_multirank(bc, oracle_c):
             buckets.append(bk)
             ts_r.append(t)
         be = bc.BaguaCommBackendPy(4, 0)
-        be.set_lanes(2)
+        be.set_lanes(lanes)
         be.register_ordered_buckets(buckets)
         backends.append((be, buckets))
         tensors.append(ts_r)
