@@ -153,11 +153,11 @@ __global__ __launch_bounds__(kBlock) void ring_mix_kernel(typename T::storage* _
     if constexpr (CONTIG) {  // one contiguous range per workgroup
         const int64_t tile = (int64_t)U * kBlock;
         const int64_t per = ((nvec + gridDim.x - 1) / gridDim.x + tile - 1) / tile * tile;
-        const int64_t lo = (int64_t)blockIdx.x * per;
-        const int64_t hi = lo + per < nvec ? lo + per : nvec;
-        int64_t base = lo;
-        for (; base + tile <= hi; base += tile) batch(base + threadIdx.x, kBlock);
-        for (int64_t u = base + threadIdx.x; u < hi; u += kBlock)
+        const int64_t v0 = (int64_t)blockIdx.x * per;  // (not lo / hi: those are the min/max keys)
+        const int64_t v1 = v0 + per < nvec ? v0 + per : nvec;
+        int64_t base = v0;
+        for (; base + tile <= v1; base += tile) batch(base + threadIdx.x, kBlock);
+        for (int64_t u = base + threadIdx.x; u < v1; u += kBlock)
             body(u, ld(t4, u), ld(l4, u), ld(r4, u), ld(w4, u));
     } else if constexpr (TILES) {
         const int64_t tile = (int64_t)U * kBlock;
