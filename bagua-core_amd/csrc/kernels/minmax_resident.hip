@@ -225,7 +225,7 @@ __device__ __forceinline__ bool sweep_chunk(const ResidentArgs& a, int cl, uint3
             hi = wave_umin(h);
             return true;
         }
-        if (bounded && wall_clock64() > deadline) return false;
+        if (bounded && (uint64_t)wall_clock64() > deadline) return false;
         __builtin_amdgcn_s_sleep(2);
     }
 }

@@ -337,7 +337,7 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_kernel(
     const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int p, typename T::storage* __restrict__ chunk,
     uint8_t* __restrict__ out_seg, float* __restrict__ part) {
     __shared__ float pos[kMaxFusedChunks], neg[kMaxFusedChunks];
-    if (threadIdx.x < p) {  // segment c decodes to +-scale_c as stored in T
+    if (threadIdx.x < (unsigned)p) {  // segment c decodes to +-scale_c as stored in T
         float sc;
         __builtin_memcpy(&sc, in + (int64_t)threadIdx.x * chunk_offset, 4);
         pos[threadIdx.x] = as_stored<T>(sc);
@@ -488,7 +488,7 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
     constexpr bool WIDE = PMAX > 8;
     __shared__ float pos[kMaxFusedChunks], neg[kMaxFusedChunks];
     __shared__ float lut[WIDE ? 2 : 1][256];
-    if (threadIdx.x < p) {  // segment c decodes to +-scale_c as stored in T
+    if (threadIdx.x < (unsigned)p) {  // segment c decodes to +-scale_c as stored in T
         float sc;
         __builtin_memcpy(&sc, in + (int64_t)threadIdx.x * chunk_offset, 4);
         pos[threadIdx.x] = as_stored<T>(sc);
