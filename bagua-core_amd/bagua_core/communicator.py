@@ -115,6 +115,34 @@ class BaguaSingleCommunicatorPy:
     def barrier(self) -> None:
         N.check(N.C.bagua_comm_barrier(self._handle), "barrier")
 
+    # bagua-core-py/src/lib.rs:117-135,145-185: collective wrappers that no compressed op uses
+    # (outside the compressed-gradient path) -- named, so a caller gets a clear
+    # error instead of an AttributeError
+    def _outside(self, name: str):
+        raise NotImplementedError(f"{name} carries no compression and is outside the compressed-gradient path "
+                                  "this library replaces (DESIGN.md §1)")
+
+    def alltoall_v(self, send_tensor, send_counts, send_displs, recv_tensor, recv_counts, recv_displs) -> None:
+        self._outside("alltoall_v")
+
+    def gather(self, send_tensor, recv_tensor, dst: int) -> None:
+        self._outside("gather")
+
+    def gather_inplace(self, tensor, count: int, dst: int) -> None:
+        self._outside("gather_inplace")
+
+    def scatter(self, send_tensor, recv_tensor, src: int) -> None:
+        self._outside("scatter")
+
+    def scatter_inplace(self, tensor, count: int, src: int) -> None:
+        self._outside("scatter_inplace")
+
+    def reduce_scatter(self, send_tensor, recv_tensor, op: int) -> None:
+        self._outside("reduce_scatter")
+
+    def reduce_scatter_inplace(self, tensor, op: int) -> None:
+        self._outside("reduce_scatter_inplace")
+
     def synchronize(self) -> None:
         N.check(N.C.bagua_comm_synchronize(self._handle), "stream synchronize")
 

@@ -131,3 +131,31 @@ def test_bucket_mark_tensor_ready_api_without_a_gpu():
         b.mark_tensor_ready(ts[2], 0)
         assert b.ready_for_comm()
         b.reset_comm_ready()
+
+
+def test_python_surface_names_every_reference_method():
+    """Every method of the reference's Python classes (bagua-core-py/src/lib.rs:19-487) exists
+    on the mirror; the collective wrappers that no compressed op uses (alltoall_v, gather,
+    scatter, reduce_scatter) raise NotImplementedError, not AttributeError."""
+    import bagua_core as bc
+    surface = {
+        bc.BaguaSingleCommunicatorPy: "nranks rank device_id abort check_abort allreduce allreduce_inplace broadcast "
+                                      "reduce reduce_inplace send recv alltoall alltoall_inplace alltoall_v allgather "
+                                      "allgather_inplace gather gather_inplace scatter scatter_inplace reduce_scatter "
+                                      "reduce_scatter_inplace barrier generate_nccl_unique_id_str",
+        bc.BaguaTensorPy: "compress to_numpy_f32 to_numpy_u8 decompress_from data_ptr device_id num_elements "
+                          "num_elements_allocated dtype",
+        bc.BaguaCommBackendPy: "register_ordered_buckets mark_communication_ready wait_pending_comm_ops",
+        bc.BaguaBucketPy: "tensors append_python_op append_centralized_synchronous_op "
+                          "append_decentralized_synchronous_op append_low_precision_decentralized_synchronous_op "
+                          "append_decentralized_asynchronous_op print_ops clear_ops ready_for_comm reset_comm_ready",
+    }
+    for cls, names in surface.items():
+        for name in names.split():
+            assert callable(getattr(cls, name, None)), f"{cls.__name__}.{name}"
+    c = bc.BaguaSingleCommunicatorPy.__new__(bc.BaguaSingleCommunicatorPy)  # no RCCL communicator needed
+    for name, args in (("alltoall_v", (None, [], [], None, [], [])), ("gather", (None, None, 0)),
+                       ("gather_inplace", (None, 0, 0)), ("scatter", (None, None, 0)), ("scatter_inplace", (None, 0, 0)),
+                       ("reduce_scatter", (None, None, 0)), ("reduce_scatter_inplace", (None, 0))):
+        with pytest.raises(NotImplementedError):
+            getattr(c, name)(*args)
