@@ -230,6 +230,7 @@ CORE_SIGNATURES = {
     "bagua_comm_backend_mark_communication_ready_desc": (_i32, [_vp, ctypes.c_char_p, _u64, _T]),
     "bagua_comm_backend_wait_pending_comm_ops": (_i32, [_vp, ctypes.POINTER(_i32)]),
     "bagua_comm_backend_failures": (_i32, [_vp]),
+    "bagua_comm_backend_stuck": (_i32, [_vp]),
     "bagua_comm_schedule_config": (_i32, [_vp, ctypes.POINTER(ctypes.c_int32), _i32]),
     "bagua_comm_backend_failure_message": (_i32, [_vp, _i32, ctypes.c_char_p, _sz]),
     "bagua_comm_backend_set_op_timeout_ms": (_i32, [_vp, ctypes.c_int64]),

@@ -24,6 +24,11 @@ from .tensor import _DTYPES, BaguaTensorPy
 
 _backend_mark = N.FAST.backend_mark
 
+# Buckets of a backend destroyed while an aborted op's worker call never returned: the
+# native side leaves that worker (and the backend) running, so what it may still touch
+# -- the buckets, their ops, tensors and communicators -- is kept here for good.
+_ABANDONED: list = []
+
 
 class BaguaCommBackendPy:
     def __init__(self, schedule_channel_cap: int, device_id: int):
@@ -35,10 +40,13 @@ class BaguaCommBackendPy:
         self._h = int(handle)  # for the fast-path mark
         self._ordered: list[BaguaBucketPy] = []  # keeps the native buckets alive while registered
         self._names: set[str] = set()
+        self._reported = 0  # monitor messages already raised by wait_pending_comm_ops
 
     def __del__(self):
         h = getattr(self, "_handle", None)
         if h is not None and h.value:
+            if N.C.bagua_comm_backend_stuck(h) != 0:
+                _ABANDONED.append(self._ordered)
             self._h = 0
             N.C.bagua_comm_backend_destroy(h)
             self._handle = None
@@ -58,8 +66,10 @@ class BaguaCommBackendPy:
                     seen.add(t.name())
                     ptrs.add(t.data_ptr())
         N.check(rc, "register_ordered_buckets")
+        keep = N.C.bagua_comm_backend_stuck(self._handle) != 0  # see wait_pending_comm_ops
         for b in self._ordered:  # the native call waited for everything scheduled
-            b._release_retired()
+            if not keep:
+                b._release_retired()
             b._schedulers.discard(self)
         self._ordered = list(buckets)
         for b in self._ordered:
@@ -96,10 +106,16 @@ class BaguaCommBackendPy:
         """lib.rs:321-337: wait for every scheduled op; returns how many finished."""
         n = ctypes.c_int(0)
         rc = N.C.bagua_comm_backend_wait_pending_comm_ops(self._handle, ctypes.byref(n))
-        for b in self._ordered:  # nothing scheduled is left to run: cleared ops may go now
-            b._release_retired()
+        # Nothing scheduled is left to run, so cleared ops may go now -- unless an op was
+        # abandoned (aborted, its worker call never returned): that call may still touch
+        # its tensors and communicators, so every retired op stays referenced for good.
+        if N.C.bagua_comm_backend_stuck(self._handle) == 0:
+            for b in self._ordered:
+                b._release_retired()
         if rc:
-            why = "; ".join(self.failures())
+            msgs = self.failures()
+            why = "; ".join(msgs[self._reported:])  # only failures not raised before
+            self._reported = len(msgs)
             raise RuntimeError(f"comm op failed: {N.STATUS.get(rc, rc)} ({n.value} ops waited for)"
                                + (f": {why}" if why else ""))
         return n.value

@@ -337,6 +337,8 @@ struct BaguaCommBackendC {
     std::vector<std::shared_ptr<Scheduled>> stuck;  // abandoned items (their worker call never returned)
     std::chrono::milliseconds op_timeout{300000};  // lib.rs:255-265 (BAGUA_COMM_OP_TIMEOUT_S)
     bool stop = false;
+    bool worker_done = false;   // work() returned (destroy waits for it, or leaves a stuck worker)
+    bool stop_monitor = false;  // the monitor outlives `stop` until the worker is done or left
     bool async = true;                  // BAGUA_BACKEND_SYNC=1: every op waits for its stream
     // BAGUA_SCHED_LANES (async only; 1 = every bucket on the comm's stream).  3: 32 x 25 MiB at
     // one rank 1,521-1,582 GiB/s vs 1,373-1,475 with 2 and 1,380-1,419 with 4
@@ -445,6 +447,9 @@ struct BaguaCommBackendC {
                 if (channel.empty()) {  // stopping with nothing queued
                     lk.unlock();
                     cover_uncovered();
+                    lk.lock();
+                    worker_done = true;
+                    cv_done.notify_all();
                     return;
                 }
                 item = channel.front();
@@ -500,12 +505,12 @@ struct BaguaCommBackendC {
 
     void watch() {
         std::unique_lock<std::mutex> lk(mu);
-        while (!stop) {
+        while (!stop_monitor) {
             // tick: a quarter of the limit, between 10 ms and 5 s
             const auto tick = std::max(std::chrono::milliseconds(10),
                                        std::min(std::chrono::milliseconds(5000), op_timeout / 4));
             cv_watch.wait_for(lk, tick);
-            if (stop) break;
+            if (stop_monitor) break;
             const auto now = std::chrono::steady_clock::now();
             std::vector<std::shared_ptr<Scheduled>> expired;
             for (auto it = inflight.begin(); it != inflight.end();) {
@@ -702,7 +707,8 @@ BaguaCommBackendC* bagua_comm_backend_create(size_t schedule_channel_cap, int de
     const char* ln = std::getenv("BAGUA_SCHED_LANES");
     if (ln && *ln) be->lanes = std::max(1, std::min(8, std::atoi(ln)));
     const char* to = std::getenv("BAGUA_COMM_OP_TIMEOUT_S");
-    if (to && *to && std::atof(to) > 0) be->op_timeout = std::chrono::milliseconds((long long)(std::atof(to) * 1000));
+    if (to && *to && std::atof(to) > 0)  // at least 1 ms, as bagua_comm_backend_set_op_timeout_ms
+        be->op_timeout = std::chrono::milliseconds(std::max(1LL, (long long)(std::atof(to) * 1000)));
     const char* prof = std::getenv("BAGUA_SCHED_PROFILE");
     be->profile = prof && *prof && std::atoi(prof) != 0;
     be->worker = std::thread([be] { be->work(); });
@@ -718,10 +724,32 @@ void bagua_comm_backend_destroy(BaguaCommBackendC* be) {
     }
     be->cv_work.notify_all();
     be->cv_space.notify_all();
+    // The worker drains what is queued, then exits; the monitor keeps watching until
+    // then, so an op stuck during the drain is still failed and aborted.  A worker whose
+    // call never returns from an aborted op (abandoned, as wait_pending_comm_ops has it)
+    // is left behind: joining it would hang, and it still uses the backend, so the
+    // backend is left allocated with it.
+    bool left = false;
+    {
+        std::unique_lock<std::mutex> lk(be->mu);
+        while (!be->worker_done) {
+            if (be->current && be->abandoned(*be->current)) {
+                left = true;
+                break;
+            }
+            be->cv_done.wait_for(lk, std::chrono::milliseconds(100));
+        }
+        be->stop_monitor = true;
+    }
     be->cv_watch.notify_all();
-    // the worker drains what is queued, then exits; enqueued work is waited for
-    if (be->worker.joinable()) be->worker.join();
     if (be->monitor.joinable()) be->monitor.join();
+    if (left) {
+        BAGUA_LOG(0, "comm backend destroyed while its worker is stuck in an aborted op: the worker and the "
+                     "backend are left behind");
+        if (be->worker.joinable()) be->worker.detach();
+        return;
+    }
+    if (be->worker.joinable()) be->worker.join();
     int n = 0;
     (void)bagua_comm_backend_wait_pending_comm_ops(be, &n);
     for (hipEvent_t e : be->spare) (void)hipEventDestroy(e);
@@ -852,6 +880,12 @@ int bagua_comm_backend_lanes(BaguaCommBackendC* be) {
     if (!be) return -1;
     std::lock_guard<std::mutex> lk(be->mu);
     return be->async ? be->lanes : 1;
+}
+
+int bagua_comm_backend_stuck(BaguaCommBackendC* be) {
+    if (!be) return -1;
+    std::lock_guard<std::mutex> lk(be->mu);
+    return (int)be->stuck.size();
 }
 
 int bagua_comm_backend_failures(BaguaCommBackendC* be) {

@@ -36,6 +36,9 @@ struct Transport {
     virtual int group_start() = 0;
     virtual int group_end() = 0;
     virtual int abort() = 0;
+    // a call of some thread is still inside the transport (or a group bracket is open):
+    // the transport may not be freed (bagua_single_communicator_c_destroy keeps it)
+    virtual bool in_use() const { return false; }
 };
 
 Transport* make_rccl_transport(ncclComm_t comm);

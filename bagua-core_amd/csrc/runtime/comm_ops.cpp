@@ -332,6 +332,12 @@ int op_schedule(const BaguaSingleCommunicatorC* c, int count, int caller) {
 // match (which over RCCL hangs; centralized_low_precision_synchronous.rs:30-71 is
 // the sequence every rank must post alike).  Costs one small allgather and a host
 // round trip per op.
+//
+// The op number assumes ONE issuing thread per communicator (its lane views count on
+// the parent): ops issued concurrently from several threads could number differently
+// on different ranks and report a false mismatch.  A stream being captured into a HIP
+// graph cannot be synchronised, so the check is refused there (BAGUA_ERR_UNSUPPORTED)
+// rather than breaking the capture.
 constexpr int kDescFields = 10;
 const char* const kDescName[kDescFields] = {"op",       "method",         "dtype",   "nranks",  "chunk elements",
                                             "num_elem", "num_elem_alloc", "schedule", "average", "op number"};
@@ -339,6 +345,12 @@ const char* const kDescName[kDescFields] = {"op",       "method",         "dtype
 int check_schedule(BaguaSingleCommunicatorC* c, int op, int method, const bagua_tensor_t* t, uint64_t chunk,
                    int sched, int average) {
     if (!c->cfg.check || c->nranks <= 1) return BAGUA_OK;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(c->stream, &cap) != hipSuccess) return BAGUA_ERR_HIP;
+    if (cap != hipStreamCaptureStatusNone) {
+        BAGUA_LOG(0, "BAGUA_CHECK_SCHEDULE: the op's stream is being captured; the check needs a host round trip");
+        return BAGUA_ERR_UNSUPPORTED;
+    }
     BaguaSingleCommunicatorC* root = c->parent ? c->parent : c;
     const int64_t mine[kDescFields] = {op, method, t->dtype, (int64_t)c->nranks, (int64_t)chunk, (int64_t)t->num_elem,
                                        (int64_t)t->num_elem_allocated, sched, average != 0,

@@ -90,7 +90,11 @@ class RcclTransport final : public Transport {
    public:
     explicit RcclTransport(ncclComm_t c) : comm_(c) {}
     ~RcclTransport() override {
-        if (comm_ && !aborted_.load()) (void)ncclCommDestroy(comm_);
+        if (!comm_) return;
+        if (!aborted_.load())
+            (void)ncclCommDestroy(comm_);
+        else
+            (void)release_if_idle();  // an abort deferred until now (the owner checked in_use())
     }
     int allreduce(const void* s, void* r, size_t n, int d, int op, hipStream_t st) override {
         Call g(this);
@@ -121,34 +125,71 @@ class RcclTransport final : public Transport {
         Call g(this);
         return g.ok ? nccl_status(ncclRecv(b, n, nccl_dtype(d), peer, comm_, st)) : BAGUA_ERR_ABORTED;
     }
-    // group brackets stay balanced after an abort (the calls between them fail)
-    int group_start() override { return nccl_status(ncclGroupStart()); }
-    int group_end() override { return nccl_status(ncclGroupEnd()); }
+    // Group brackets stay balanced after an abort (the calls between them fail).  An
+    // open bracket counts as use: ncclGroupEnd runs the grouped sends/recvs against the
+    // communicator, so it may not be freed between a grouped call and its group end.
+    int group_start() override {
+        depth_.fetch_add(1);
+        return nccl_status(ncclGroupStart());
+    }
+    int group_end() override {
+        int rc;
+        {
+            Call g(this);  // inside RCCL while the group's tasks are issued
+            rc = nccl_status(ncclGroupEnd());
+            depth_.fetch_sub(1);
+        }
+        return rc;
+    }
     // From any thread (the scheduler's monitor aborts a stuck op's communicator while
-    // the worker may be enqueueing): later calls fail with BAGUA_ERR_ABORTED; calls
-    // already inside RCCL get up to 2 s to return before ncclCommAbort frees the
-    // communicator -- a call blocked longer is what the abort is there to release.
+    // the worker may be enqueueing).  Later calls fail with BAGUA_ERR_ABORTED at once.
+    // ncclCommAbort, which frees the communicator, runs only when no call is inside RCCL
+    // and no group bracket is open: right away, after up to 2 s for a call that is about
+    // to return, or else deferred to the moment the last such call returns (a call
+    // blocked on a peer returns when that peer's process ends or the peer posts) or to
+    // the transport's destruction.  The communicator is never freed under a call.
     int abort() override {
         if (aborted_.exchange(true)) return BAGUA_OK;
         const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(2);
-        while (inflight_.load() > 0 && std::chrono::steady_clock::now() < until)
+        while (in_use() && std::chrono::steady_clock::now() < until)
             std::this_thread::sleep_for(std::chrono::milliseconds(1));
-        return comm_ ? nccl_status(ncclCommAbort(comm_)) : BAGUA_OK;
+        const int rc = release_if_idle();
+        if (!released_.load())
+            BAGUA_LOG(1, "communicator abort deferred: a call is still inside RCCL; the communicator is "
+                         "released when it returns");
+        return rc;
     }
+    bool in_use() const override { return inflight_.load() > 0 || depth_.load() > 0; }
 
    private:
+    // ncclCommAbort once, by whichever thread finds the transport aborted and idle
+    int release_if_idle() {
+        std::lock_guard<std::mutex> g(release_mu_);
+        if (released_.load() || !comm_ || in_use()) return BAGUA_OK;
+        released_.store(true);
+        return nccl_status(ncclCommAbort(comm_));
+    }
+    // A call enters (inflight_ first, then the flag) while abort() sets the flag first,
+    // then reads inflight_: with sequentially consistent atomics either the call sees
+    // the abort and stays out of RCCL, or the abort sees the call and defers.
     struct Call {
         explicit Call(RcclTransport* t) : t_(t) {
             t_->inflight_.fetch_add(1);
             ok = !t_->aborted_.load() && t_->comm_;
         }
-        ~Call() { t_->inflight_.fetch_sub(1); }
+        ~Call() {
+            t_->inflight_.fetch_sub(1);
+            if (t_->aborted_.load()) (void)t_->release_if_idle();
+        }
         RcclTransport* t_;
         bool ok = false;
     };
     ncclComm_t comm_;
     std::atomic<bool> aborted_{false};
+    std::atomic<bool> released_{false};
     std::atomic<int> inflight_{0};
+    std::atomic<int> depth_{0};
+    std::mutex release_mu_;
 };
 
 Transport* make_rccl_transport(ncclComm_t comm) { return new RcclTransport(comm); }
@@ -275,9 +316,16 @@ void bagua_single_communicator_c_destroy(BaguaSingleCommunicatorC** ptr) {
     if (!ptr || !*ptr) return;
     BaguaSingleCommunicatorC* c = *ptr;
     if (c->t && c->aborted.load()) c->t->abort();
+    *ptr = nullptr;
+    if (c->t && c->t->in_use()) {
+        // a thread is still inside an (aborted) call on this communicator: freeing it, or
+        // its transport, would pull them from under that call -- both are kept
+        BAGUA_LOG(0, "communicator rank %zu/%zu destroyed while a call is still inside it: kept", c->rank,
+                  c->nranks);
+        return;
+    }
     delete c->t;
     delete c;
-    *ptr = nullptr;
 }
 
 int32_t bagua_single_communicator_c_nranks(BaguaSingleCommunicatorC** ptr, size_t* nranks) {

@@ -22,7 +22,9 @@
 // a rank waiting for a peer that never comes returns at once.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <mutex>
 #include <vector>
@@ -59,8 +61,15 @@ const char* kind_name(int k) {
 
 struct LoopbackGroup {
     explicit LoopbackGroup(int n, int dev)
-        : p(n), device(dev), cfg(read_schedule_config()), ptr(n), desc(n), sends(n), recvs(n) {}
+        : p(n), device(dev), cfg(read_schedule_config()), ptr(n), desc(n), sends(n), recvs(n) {
+        // test hook: BAGUA_LOOPBACK_ABORT_HOLD_S=<s> makes abort() leave a waiting rank
+        // waiting for <s> seconds instead of releasing it, as a transport whose blocked
+        // call never returns (the scheduler must then leave the call behind, not hang)
+        const char* h = std::getenv("BAGUA_LOOPBACK_ABORT_HOLD_S");
+        hold_s = h && *h ? std::atoi(h) : 0;
+    }
     int p, device;
+    int hold_s = 0;
     ScheduleConfig cfg;  // one process: every virtual rank reads the same environment, once
     std::mutex mu;
     std::condition_variable cv;
@@ -72,6 +81,7 @@ struct LoopbackGroup {
     std::vector<std::vector<Post>> sends, recvs;
 
     void break_all() {
+        if (hold_s > 0) return;  // the test hook: a waiting rank stays inside its call
         std::lock_guard<std::mutex> lk(mu);
         broken = true;
         cv.notify_all();
@@ -87,7 +97,8 @@ struct LoopbackGroup {
             cv.notify_all();
             return true;
         }
-        if (!cv.wait_for(lk, std::chrono::seconds(60), [&] { return gen != my || broken; }) || broken) {
+        const auto limit = std::chrono::seconds(hold_s > 0 ? hold_s : 60);
+        if (!cv.wait_for(lk, limit, [&] { return gen != my || broken; }) || broken) {
             broken = true;
             cv.notify_all();
             return false;
@@ -97,10 +108,20 @@ struct LoopbackGroup {
 };
 
 class LoopbackTransport final : public Transport {
+    // a call in progress (the owner may not free the transport under it)
+    struct Busy {
+        explicit Busy(LoopbackTransport* t) : t_(t) { t_->inflight_.fetch_add(1); }
+        ~Busy() { t_->inflight_.fetch_sub(1); }
+        LoopbackTransport* t_;
+    };
+    std::atomic<int> inflight_{0};
+
    public:
     LoopbackTransport(LoopbackGroup* g, int rank) : g_(g), r_(rank) {}
+    bool in_use() const override { return inflight_.load() > 0 || in_group_; }
 
     int alltoall(const void* s, void* rcv, size_t n, int d, hipStream_t st) override {
+        Busy busy(this);
         const size_t b = n * bagua_dtype_bytes(d);
         if (int rc = enter(st, s, kAllToAll, b)) return rc;
         for (int j = 0; j < g_->p; ++j)
@@ -108,6 +129,7 @@ class LoopbackTransport final : public Transport {
         return leave(st);
     }
     int allgather(const void* s, void* rcv, size_t n, int d, hipStream_t st) override {
+        Busy busy(this);
         const size_t b = n * bagua_dtype_bytes(d);
         if (int rc = enter(st, s, kAllGather, b)) return rc;
         for (int j = 0; j < g_->p; ++j) {
@@ -118,12 +140,14 @@ class LoopbackTransport final : public Transport {
         return leave(st);
     }
     int broadcast(void* buf, size_t n, int d, int root, hipStream_t st) override {
+        Busy busy(this);
         const size_t b = n * bagua_dtype_bytes(d);
         if (int rc = enter(st, buf, kBroadcast, b, root)) return rc;
         if (r_ != root && copy(buf, g_->ptr[root], b, st)) return BAGUA_ERR_HIP;
         return leave(st);
     }
     int allreduce(const void* s, void* rcv, size_t n, int d, int op, hipStream_t st) override {
+        Busy busy(this);
         // SUM / AVG over ranks in rank order (test transport; not bit-matched to RCCL)
         if (op != BAGUA_OP_SUM && op != BAGUA_OP_AVG) return BAGUA_ERR_UNSUPPORTED;
         const size_t b = n * bagua_dtype_bytes(d);
@@ -139,6 +163,7 @@ class LoopbackTransport final : public Transport {
         return hipStreamSynchronize(st) == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP;
     }
     int reduce(const void* s, void* rcv, size_t n, int d, int op, int root, hipStream_t st) override {
+        Busy busy(this);
         // SUM / AVG over ranks in rank order on the root; the others only contribute
         if (op != BAGUA_OP_SUM && op != BAGUA_OP_AVG) return BAGUA_ERR_UNSUPPORTED;
         const size_t b = n * bagua_dtype_bytes(d);
@@ -157,10 +182,12 @@ class LoopbackTransport final : public Transport {
         return hipStreamSynchronize(st) == hipSuccess ? BAGUA_OK : BAGUA_ERR_HIP;
     }
     int send(const void* buf, size_t n, int d, int peer, hipStream_t st) override {
+        Busy busy(this);
         my_sends_.push_back({peer, const_cast<void*>(buf), n * bagua_dtype_bytes(d)});
         return in_group_ ? BAGUA_OK : flush(st);
     }
     int recv(void* buf, size_t n, int d, int peer, hipStream_t st) override {
+        Busy busy(this);
         my_recvs_.push_back({peer, buf, n * bagua_dtype_bytes(d)});
         stream_ = st;
         return in_group_ ? BAGUA_OK : flush(st);
@@ -170,6 +197,7 @@ class LoopbackTransport final : public Transport {
         return BAGUA_OK;
     }
     int group_end() override {
+        Busy busy(this);
         in_group_ = false;
         return flush(stream_);
     }
@@ -260,7 +288,7 @@ class LoopbackTransport final : public Transport {
 
     LoopbackGroup* g_;
     int r_;
-    bool in_group_ = false;
+    std::atomic<bool> in_group_{false};
     uint64_t seq_ = 0;  // collectives this rank posted
     hipStream_t stream_ = nullptr;
     std::vector<Post> my_sends_, my_recvs_;

@@ -146,6 +146,7 @@ METRIC = ("GiB/s fp32 gradient encode+decode (device-resident); "
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GiB = float(1 << 30)
 SIDE_TIMEOUT_S = 120.0  # N > 1 side measurements: abort the communicator instead of hanging
+MIN_SIDE_S = 10.0  # N > 1: a side line starts only with this much of --budget-s left
 HEADLINE_TIMEOUT_S = 300.0  # N > 1 headline (pipelined op): abort, then measure the unpieced op
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")
 PMC_SUMMARY_ONEBIT = os.path.join(ROOT, "profiles", "r05_pmc_traffic_onebit.json")
@@ -179,6 +180,10 @@ def parse():
     ap.add_argument("--copy-chunks", type=int, default=2,
                     help="host workload: pieces per H2D / D2H copy (1 = one copy each way per bucket)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the cpu_baseline leg")
+    ap.add_argument("--budget-s", type=float, default=420.0,
+                    help="N > 1: wall budget of the whole line from process start; the headline, the fp32 "
+                         "all-reduce and comm-only always run, later side lines are skipped once it is spent "
+                         "(skipped_for_budget)")
     ap.add_argument("--kernel-events-every", type=int, default=5,
                     help="codec workloads: the dominant kernel records start/stop events on every N-th timed step")
     ap.add_argument("--stream", choices=["own", "current"], default="own",
@@ -836,23 +841,41 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         return float(t.item()) / steps
 
     side_errors = {}
+    skipped = []  # side lines not started because the line's wall budget was spent
 
-    def side(name, fn):
+    def remaining_s() -> float:
+        # the line's wall budget left, the same on every rank (min over ranks, gloo), so
+        # every rank skips the same side lines
+        left = torch.tensor([args.budget_s - (time.perf_counter() - _PROCESS_T0)], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(left, op=dist.ReduceOp.MIN)
+        return float(left.item())
+
+    def side(name, fn, required=False):
         # side measurements must not cost the headline line: an error that every rank
         # raises alike (argument checks, an unsupported shape) is recorded instead, and a
-        # measurement that has not finished after SIDE_TIMEOUT_S aborts the communicator
+        # measurement that has not finished after its limit aborts the communicator
         # (ncclCommAbort: pending collectives return) so the line is still printed; the
-        # ranks then agree (gloo) to rebuild it, so the later side lines still measure
+        # ranks then agree (gloo) to rebuild it, so the later side lines still measure.
+        # The limit is SIDE_TIMEOUT_S or what is left of --budget-s, whichever is less; a
+        # line that is not `required` is skipped (skipped_for_budget) once less than
+        # MIN_SIDE_S is left.
         nonlocal comm
         expired = []
+        left = remaining_s()
+        if not required and left < MIN_SIDE_S:
+            skipped.append(name)
+            return float("nan")
 
         # test hook (BAGUA_BENCH_FAIL_SIDE=<side line>): that line's limit is 0 s, so its
         # communicator is aborted at once and the recovery below runs
-        limit = 0.0 if os.environ.get("BAGUA_BENCH_FAIL_SIDE") == name else SIDE_TIMEOUT_S
+        limit = SIDE_TIMEOUT_S if required else max(MIN_SIDE_S, min(SIDE_TIMEOUT_S, left))
+        if os.environ.get("BAGUA_BENCH_FAIL_SIDE") == name:
+            limit = 0.0
 
         def expire():
             expired.append(True)
-            side_errors[name] = f"timed out after {limit} s; communicator aborted and rebuilt"
+            side_errors[name] = f"timed out after {limit:.0f} s; communicator aborted and rebuilt"
             comm.abort()
 
         timer = threading.Timer(limit, expire)
@@ -875,11 +898,19 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             return float("nan")
         return res
 
+    def budget_allows(name) -> bool:
+        """a block of side lines with set-up of its own starts only with MIN_SIDE_S left"""
+        if remaining_s() >= MIN_SIDE_S:
+            return True
+        skipped.append(name)
+        return False
+
     # The headline: the pipelined op.  Its multi-group RCCL schedule has run over the
     # loopback transport, gloo and single-rank RCCL only (DESIGN.md §6); should it not
-    # finish on this node within HEADLINE_TIMEOUT_S, the communicator is aborted and
-    # the headline falls back to the unpieced op (the reference's one alltoall + one
-    # allgather) on a fresh communicator, recorded in headline_fallback.
+    # finish on this node within its limit (HEADLINE_TIMEOUT_S, at most half the line's
+    # budget), the communicator is aborted and the headline falls back to the unpieced
+    # op (the reference's one alltoall + one allgather) on a fresh communicator,
+    # recorded in headline_fallback.
     headline_fallback = None
     aborted = []
     autotune = {}  # pieces -> s per step during the untimed choice (N > 1, --pieces 0)
@@ -889,7 +920,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         aborted.append(True)
         comm.abort()
 
-    timer = threading.Timer(HEADLINE_TIMEOUT_S, expire_headline)
+    timer = threading.Timer(max(30.0, min(HEADLINE_TIMEOUT_S, 0.5 * args.budget_s)), expire_headline)
     timer.daemon = True
     timer.start()
     try:
@@ -900,7 +931,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             # steps at each count, the fastest max-over-ranks time wins on every rank alike
             for q in (1, 2, 4, 8, 16):
                 autotune[str(q)] = timed(lambda q=q: compressed_step(q), 2, 1)
-            for q in (4, 8):  # first and last piece half size: shorter prefix and suffix (DESIGN.md §9)
+            for q in (4, 8):  # first and last piece half size: shorter prefix and suffix (DESIGN.md §6)
                 autotune[f"{q}_tapered"] = timed(lambda q=q: compressed_step(q, taper=True), 2, 1)
             best = min(autotune, key=lambda q: autotune[q])
             args.pieces = int(best.split("_")[0])
@@ -925,33 +956,13 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         args.pieces = 1
         t_c = timed(lambda: compressed_step(1), args.steps, args.warmup)
     PHASES.lap("headline")
-    t_u = side("unpieced", lambda: compressed_step(1))
-    PHASES.lap("unpieced")
-    # piece counts either side of the automatic choice (4 per chunk at 1 GiB), so the node's own
-    # run says which count hides the codec best behind its links
-    sweep = {}
-    if world > 1 and not headline_fallback:
-        for q in (2, 8):
-            sweep[str(q)] = side(f"pieces_{q}", lambda q=q: compressed_step(q))
-
-        def tapered(q):
-            # first and last piece half size (N.PIECES_TAPERED, minmax_u8.hip piece_range)
-            compressed_step(q, taper=True)
-
-        for q in (4, 5):
-            sweep[f"{q}_tapered"] = side(f"pieces_{q}_tapered", lambda q=q: tapered(q))
-        PHASES.lap("pieces_sweep")
-    t_f = side("fp32_allreduce", fp32_step)
-    PHASES.lap("fp32_allreduce")
-    # the same all-reduce with the 1-bit sign+scale codec (this repo's extension:
-    # N/8 wire bytes per phase instead of N), fused middle step
-    def onebit_step(pieces=user_pieces):
-        N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
-                                                              N.COMPRESSION_ONEBIT, pieces), "1-bit allreduce")
-
-    # decomposition: the op's two collectives alone on its compressed bytes (RCCL alltoall of
-    # S bytes, in-place allgather of S bytes), so the codec time the op did not hide is
+    # What the north star compares the headline with, measured right after it (never
+    # skipped for the budget): the uncompressed fp32 RCCL all-reduce of the same bucket,
+    # and the op's two collectives alone on its compressed bytes (RCCL alltoall of S
+    # bytes, in-place allgather of S bytes), so the codec time the op did not hide is
     # ms_per_step - comm_only_ms
+    t_f = side("fp32_allreduce", fp32_step, required=True)
+    PHASES.lap("fp32_allreduce")
     S_c = N.K.bagua_minmax_u8_compressed_bytes(0, n // world, world)
     cbuf = [torch.zeros(S_c, dtype=torch.uint8, device=dev) for _ in range(2)]
     craw = [N.bagua_tensor_t(b.data_ptr(), S_c, S_c, 3, local_rank) for b in cbuf]
@@ -961,9 +972,19 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         N.check(N.C.bagua_comm_allgather_inplace(comm.handle, ctypes.byref(craw[1])), "allgather")
         N.check(N.C.bagua_comm_synchronize(comm.handle), "sync")
 
-    t_comm = side("comm_only", comm_only)
+    t_comm = side("comm_only", comm_only, required=True)
     del cbuf, craw
     PHASES.lap("comm_only")
+    # the same all-reduce with the 1-bit sign+scale codec (this repo's extension:
+    # N/8 wire bytes per phase instead of N), fused middle step
+    def onebit_step(pieces=user_pieces):
+        N.check(N.C.bagua_centralized_low_precision_pipelined(comm.handle, ctypes.byref(raw), 1,
+                                                              N.COMPRESSION_ONEBIT, pieces), "1-bit allreduce")
+
+    t_o = side("onebit", onebit_step)
+    PHASES.lap("onebit")
+    t_u = side("unpieced", lambda: compressed_step(1))
+    PHASES.lap("unpieced")
     # Bagua's default bucket size (25 MiB of fp32): the same op and the fp32 all-reduce on the
     # first 25 MiB of the bucket, where latency, not bandwidth, sets the step
     m = min(n, (25 << 20) // 4)
@@ -974,34 +995,8 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
     t_sf = side("bucket_25mib_fp32", lambda: N.check(N.C.bagua_centralized_full_precision_synchronous(
         comm.handle, ctypes.byref(small), 1), "25 MiB fp32 allreduce"))
     PHASES.lap("bucket_25mib")
-    # the scheduler workload (32 x 25 MiB buckets, Bagua's default bucket size) through the native
-    # scheduler on this communicator: cross-bucket lanes (the default) and one lane, so the node's
-    # run shows how much of each bucket's codec prefix the next bucket's exchange hides
-    sched = {}
-    nbk, mib = (32, 25) if not args.elements else (8, max(1, (4 * n >> 20) // 8))  # --elements: a rehearsal
-    if world > 1:
-        try:
-            wl = SchedulerWorkload(comm, world, rank, local_rank, nbk, mib)
-            sched["buckets"], sched["bucket_mib"] = nbk, mib
-            for ln in (wl.backend.lanes(), 1):
-                if wl.comm is not comm:  # a timed-out side line rebuilt the communicator
-                    wl.close()
-                    wl = SchedulerWorkload(comm, world, rank, local_rank, nbk, mib)
-                wl.backend.set_lanes(ln)
-                t_sc = side(f"scheduler_lanes{ln}", wl.iteration)
-                sched[f"lanes_{ln}"] = {"ms_per_step": round(t_sc * 1e3, 4),
-                                        "per_bucket_us": round(t_sc * 1e6 / nbk, 2),
-                                        "gib_s_total": round(world * 4.0 * wl.per * nbk / t_sc / GiB, 2)}
-            wl.close()
-            del wl
-        except Exception as e:  # noqa: BLE001 - a failed side measurement must not lose the headline line
-            side_errors.setdefault("scheduler", str(e)[:200])
-        PHASES.lap("scheduler_buckets")
-    t_o = side("onebit", onebit_step)
-    t_ou = side("onebit_unpieced", lambda: onebit_step(1))
-    PHASES.lap("onebit")
     decentralized = None
-    if not args.no_decentralized:
+    if not args.no_decentralized and budget_allows("decentralized"):
         # config 5: bf16 bucket, decentralized ring exchange with the uint8 codec
         # (decentralized_low_precision_synchronous.rs:42-152), 2^27 elements per rank
         try:
@@ -1019,8 +1014,8 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
 
             multipath = world >= 6  # comm_ops.cpp kRingMinMultipath
             t_d = side("decentralized", dec_step)
-            t_dm = side("decentralized_multipath", lambda: dec_step(multipath=True)) if multipath else float("nan")
             t_du = side("decentralized_unpieced", lambda: dec_step(1))
+            t_dm = side("decentralized_multipath", lambda: dec_step(multipath=True)) if multipath else float("nan")
             decentralized = {"config_index": 5, "elements_per_rank": nb, "dtype": "bf16",
                              "exchange": "direct (the reference's; multipath is opt-in)",
                              "ms_per_step": round(t_d * 1e3, 3), "unpieced_ms_per_step": round(t_du * 1e3, 3),
@@ -1031,6 +1026,51 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         except Exception as e:  # noqa: BLE001 - a failed side measurement must not lose the headline line
             decentralized = {"error": str(e)[:200]}
         PHASES.lap("decentralized_bf16")
+    t_ou = side("onebit_unpieced", lambda: onebit_step(1))
+    PHASES.lap("onebit_unpieced")
+    # the scheduler workload (32 x 25 MiB buckets, Bagua's default bucket size) through the native
+    # scheduler on this communicator: cross-bucket lanes (the library default, 3) and one lane;
+    # the faster of the two on this node is recorded as lanes_chosen (the library
+    # default stays 3 only while a node line shows lanes paying at p > 1)
+    sched = {}
+    nbk, mib = (32, 25) if not args.elements else (8, max(1, (4 * n >> 20) // 8))  # --elements: a rehearsal
+    if world > 1 and budget_allows("scheduler_buckets"):
+        try:
+            wl = SchedulerWorkload(comm, world, rank, local_rank, nbk, mib)
+            sched["buckets"], sched["bucket_mib"] = nbk, mib
+            for ln in (wl.backend.lanes(), 1):
+                if wl.comm is not comm:  # a timed-out side line rebuilt the communicator
+                    wl.close()
+                    wl = SchedulerWorkload(comm, world, rank, local_rank, nbk, mib)
+                wl.backend.set_lanes(ln)
+                t_sc = side(f"scheduler_lanes{ln}", wl.iteration)
+                if math.isfinite(t_sc):
+                    sched[f"lanes_{ln}"] = {"ms_per_step": round(t_sc * 1e3, 4),
+                                            "per_bucket_us": round(t_sc * 1e6 / nbk, 2),
+                                            "gib_s_total": round(world * 4.0 * wl.per * nbk / t_sc / GiB, 2)}
+            timed_lanes = {int(k[6:]): v["ms_per_step"] for k, v in sched.items() if k.startswith("lanes_")}
+            if timed_lanes:
+                sched["lanes_chosen"] = min(timed_lanes, key=timed_lanes.get)
+            wl.close()
+            del wl
+        except Exception as e:  # noqa: BLE001 - a failed side measurement must not lose the headline line
+            side_errors.setdefault("scheduler", str(e)[:200])
+        PHASES.lap("scheduler_buckets")
+    # piece counts either side of the automatic choice (the autotune already timed them
+    # briefly), so the node's own run says which count hides the codec best behind its links
+    sweep = {}
+    if world > 1 and not headline_fallback:
+        for q in (2, 8):
+            sweep[str(q)] = side(f"pieces_{q}", lambda q=q: compressed_step(q))
+
+        def tapered(q):
+            # first and last piece half size (N.PIECES_TAPERED, minmax_u8.hip piece_range)
+            compressed_step(q, taper=True)
+
+        for q in (4, 5):
+            sweep[f"{q}_tapered"] = side(f"pieces_{q}_tapered", lambda q=q: tapered(q))
+        sweep = {q: v for q, v in sweep.items() if math.isfinite(v)}
+        PHASES.lap("pieces_sweep")
     value = world * 4.0 * n / t_c / GiB
     per_rank = 4.0 * n / t_c / GiB
     fp32 = 4.0 * n / t_f / GiB
@@ -1097,6 +1137,8 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
              "per_kernel_us": {nm: round(t * 1e3, 2) for nm, t in zip(names, per)}}
     if side_errors:
         extra["side_errors"] = side_errors
+    extra["budget_s"] = args.budget_s
+    extra["skipped_for_budget"] = skipped
     if headline_fallback:
         extra["headline_fallback"] = headline_fallback
     del comm
@@ -1276,6 +1318,9 @@ def main():
         # after every rank's timed region: rank 0 times the op on the host cores while
         # the others wait at the closing barrier
         if rank == 0 and not args.no_cpu_baseline:
+            if workload == "allreduce" and world > 1:  # inside the line's wall budget too
+                left = args.budget_s - (time.perf_counter() - _PROCESS_T0)
+                args.cpu_seconds = max(0.5, min(args.cpu_seconds, left - 10.0))
             try:
                 cpu = cpu_allreduce_baseline(args, world, n_cpu, torch.device("cuda", local_rank))
             except Exception as e:  # noqa: BLE001 - a failed baseline must not lose the headline line

@@ -320,6 +320,11 @@ int bagua_comm_backend_wait_pending_comm_ops(BaguaCommBackendC* backend, int* co
  * failure_message copies message i into buf (NUL-terminated, truncated to len) and
  * returns its full length, -1 when there is no message i. */
 int bagua_comm_backend_failures(BaguaCommBackendC* backend);
+/* Ops abandoned by wait_pending_comm_ops: aborted, and their worker call never
+ * returned.  While any exists, the buffers those ops were given must stay alive (the
+ * call may still touch them); destroy then leaves the worker and the backend behind
+ * instead of joining a thread that never returns. */
+int bagua_comm_backend_stuck(BaguaCommBackendC* backend);
 int bagua_comm_backend_failure_message(BaguaCommBackendC* backend, int i, char* buf, size_t len);
 int bagua_comm_backend_set_op_timeout_ms(BaguaCommBackendC* backend, int64_t ms);
 /* Cross-bucket pipelining (no reference counterpart): bucket i of the registration

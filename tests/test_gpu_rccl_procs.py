@@ -182,6 +182,51 @@ def test_bench_side_line_timeout_recovers(tmp_path):
     assert d["onebit_allreduce"]["ms_per_step"] > 0 and d["decentralized_bf16"]["ms_per_step"] > 0
 
 
+def test_bench_line_budget(tmp_path):
+    """The N > 1 line under a wall budget (--budget-s 20 from process start): the headline,
+    the fp32 all-reduce and comm-only always run, then side lines are skipped once fewer
+    than MIN_SIDE_S seconds are left -- the line still prints its one JSON line, with the
+    skipped lines named, inside the budget plus the closing CPU baseline's slack."""
+    import json
+    import time
+    env = dict(os.environ)
+    env.update({"BAGUA_BENCH_SHARED_GPU": "1", "NCCL_IB_DISABLE": "1", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--elements", str(1 << 22), "--cpu-seconds", "1", "--budget-s", "20"]
+    t0 = time.time()
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    wall = time.time() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["value"] > 0 and d["fp32_allreduce_gib_s"] > 0 and d["ratio_vs_fp32"] > 0, d
+    assert d["comm_only_ms"] > 0 and d["budget_s"] == 20 and "phase_wall_s" in d, d
+    assert d["skipped_for_budget"], d  # at least the trailing side lines
+    assert "side_errors" not in d, d
+    assert wall < 20 + 60, wall  # launcher + a side line started just inside the budget
+
+
+def test_bench_line_zero_budget(tmp_path):
+    """--budget-s 0: every skippable side line is skipped (decentralized and the scheduler
+    blocks included), the required ones still measure."""
+    import json
+    env = dict(os.environ)
+    env.update({"BAGUA_BENCH_SHARED_GPU": "1", "NCCL_IB_DISABLE": "1", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--elements", str(1 << 22), "--cpu-seconds", "1", "--budget-s", "0"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["value"] > 0 and d["fp32_allreduce_gib_s"] > 0 and d["comm_only_ms"] > 0, d
+    want = {"onebit", "unpieced", "bucket_25mib", "bucket_25mib_fp32", "decentralized", "onebit_unpieced",
+            "scheduler_buckets", "pieces_2", "pieces_8", "pieces_4_tapered", "pieces_5_tapered"}
+    assert set(d["skipped_for_budget"]) == want, d["skipped_for_budget"]
+    assert d["decentralized_bf16"] is None and d["scheduler_buckets"] is None, d
+
+
 @pytest.mark.parametrize("world,fail_headline,launcher", [(2, False, "self"), (8, False, "self"),
                                                           (2, True, "torchrun")])
 def test_bench_line_multirank(tmp_path, world, fail_headline, launcher):
@@ -229,7 +274,10 @@ def test_bench_line_multirank(tmp_path, world, fail_headline, launcher):
         assert all(v > 0 for v in d["pieces_sweep_ms_per_step"].values()), d["pieces_sweep_ms_per_step"]
     assert d["roofline"]["frac"] > 0
     sc = d["scheduler_buckets"]  # the native scheduler over this RCCL communicator, lanes and one lane
-    assert sc and sc["lanes_1"]["ms_per_step"] > 0 and len([k for k in sc if k.startswith("lanes_")]) == 2, sc
+    assert sc and sc["lanes_1"]["ms_per_step"] > 0 and len([k for k in sc if k.startswith("lanes_")]) == 3, sc
+    timed_lanes = {int(k[6:]): v["ms_per_step"] for k, v in sc.items() if k.startswith("lanes_") and k[6:].isdigit()}
+    assert sc["lanes_chosen"] == min(timed_lanes, key=timed_lanes.get), sc
+    assert d["skipped_for_budget"] == [] and d["budget_s"] == 420, d
     # the CPU path beside every N: rank 0 runs the op sequence for all ranks on the host cores
     c = d["cpu_baseline"]
     assert c and c["value"] > 0 and c["cores"] >= 1 and c["host"]["os_cpu_count"] >= 1 and str(world) in c["sample"]

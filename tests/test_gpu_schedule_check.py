@@ -198,3 +198,41 @@ def test_stuck_op_fails_within_limit(bc):
     t1 = time.time()
     del backend
     assert time.time() - t1 < 10
+
+
+def test_stuck_op_never_released(bc, monkeypatch):
+    """a transport whose blocked call never returns after the abort
+    (BAGUA_LOOPBACK_ABORT_HOLD_S: the loopback rank keeps waiting 20 s).  The op is failed
+    at the limit, wait_pending_comm_ops raises once the op is abandoned (10 s after the
+    abort), the backend reports it stuck and keeps the retired ops' references, and
+    destroying the backend leaves the stuck worker behind instead of joining it.  The
+    communicators outlive the hold, so the worker returns into live objects."""
+    from bagua_core import backend as backend_mod
+    from bagua_core.communicator import loopback_communicators
+    monkeypatch.setenv("BAGUA_LOOPBACK_ABORT_HOLD_S", "20")
+    comms = loopback_communicators(2, 0)
+    x = torch.randn(2 * 65536, device="cuda") * 1e-3
+    torch.cuda.synchronize()
+    bk = bc.BaguaBucketPy("held", [bc.BaguaTensorPy(x, "x")])
+    bk.append_centralized_synchronous_op(comms[0], None, False, True, False, "MinMaxUInt8")
+    backend = bc.BaguaCommBackendPy(1, 0)
+    backend.set_op_timeout(1.0)
+    backend.register_ordered_buckets([bk])
+    bk.clear_ops()  # its op is retired while scheduled: must stay referenced while stuck
+    bk.append_centralized_synchronous_op(comms[0], None, False, True, False, "MinMaxUInt8")
+    ev = torch.cuda.Event()
+    ev.record()
+    t0 = time.time()
+    backend.mark_communication_ready(bk.tensors()[0], ev.cuda_event)
+    with pytest.raises(RuntimeError, match="has not finished for 1 s"):
+        backend.wait_pending_comm_ops()
+    assert 1.0 + 10.0 <= time.time() - t0 < 20.0
+    N = bc._native
+    assert N.C.bagua_comm_backend_stuck(backend._handle) == 1
+    assert bk._retired, "the retired op must stay referenced while its call is stuck"
+    t1 = time.time()
+    del backend
+    assert time.time() - t1 < 5
+    assert backend_mod._ABANDONED and backend_mod._ABANDONED[-1][0] is bk
+    time.sleep(max(0.0, 20.0 + 3.0 - (time.time() - t0)))  # the held call has returned
+    backend_mod._ABANDONED.clear()
