@@ -182,8 +182,13 @@ def test_bench_side_line_timeout_recovers(tmp_path):
     assert d["onebit_allreduce"]["ms_per_step"] > 0 and d["decentralized_bf16"]["ms_per_step"] > 0
 
 
+# the N > 1 line's skippable side lines in the order they run (bench.py bench_allreduce)
+SIDE_ORDER = ["onebit", "unpieced", "bucket_25mib", "bucket_25mib_fp32", "decentralized", "onebit_unpieced",
+              "scheduler_buckets", "pieces_2", "pieces_8", "pieces_4_tapered", "pieces_5_tapered"]
+
+
 def test_bench_line_budget(tmp_path):
-    """The N > 1 line under a wall budget (--budget-s 20 from process start): the headline,
+    """The N > 1 line under a wall budget (--budget-s 14 from process start): the headline,
     the fp32 all-reduce and comm-only always run, then side lines are skipped once fewer
     than MIN_SIDE_S seconds are left -- the line still prints its one JSON line, with the
     skipped lines named, inside the budget plus the closing CPU baseline's slack."""
@@ -193,7 +198,7 @@ def test_bench_line_budget(tmp_path):
     env.update({"BAGUA_BENCH_SHARED_GPU": "1", "NCCL_IB_DISABLE": "1", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-           "--elements", str(1 << 22), "--cpu-seconds", "1", "--budget-s", "20"]
+           "--elements", str(1 << 26), "--cpu-seconds", "1", "--budget-s", "14"]  # 256 MiB per rank
     t0 = time.time()
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     wall = time.time() - t0
@@ -202,10 +207,11 @@ def test_bench_line_budget(tmp_path):
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["value"] > 0 and d["fp32_allreduce_gib_s"] > 0 and d["ratio_vs_fp32"] > 0, d
-    assert d["comm_only_ms"] > 0 and d["budget_s"] == 20 and "phase_wall_s" in d, d
-    assert d["skipped_for_budget"], d  # at least the trailing side lines
+    assert d["comm_only_ms"] > 0 and d["budget_s"] == 14 and "phase_wall_s" in d, d
+    skipped = d["skipped_for_budget"]
+    assert skipped and skipped == SIDE_ORDER[len(SIDE_ORDER) - len(skipped):], skipped  # a tail of the order
     assert "side_errors" not in d, d
-    assert wall < 20 + 60, wall  # launcher + a side line started just inside the budget
+    assert wall < 14 + 60, wall  # launcher + a side line started just inside the budget
 
 
 def test_bench_line_zero_budget(tmp_path):
@@ -221,9 +227,7 @@ def test_bench_line_zero_budget(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["value"] > 0 and d["fp32_allreduce_gib_s"] > 0 and d["comm_only_ms"] > 0, d
-    want = {"onebit", "unpieced", "bucket_25mib", "bucket_25mib_fp32", "decentralized", "onebit_unpieced",
-            "scheduler_buckets", "pieces_2", "pieces_8", "pieces_4_tapered", "pieces_5_tapered"}
-    assert set(d["skipped_for_budget"]) == want, d["skipped_for_budget"]
+    assert d["skipped_for_budget"] == SIDE_ORDER, d["skipped_for_budget"]
     assert d["decentralized_bf16"] is None and d["scheduler_buckets"] is None, d
 
 
