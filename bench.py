@@ -372,8 +372,13 @@ def bench_codec(args, onebit: bool = False):
     # the committed PMC passes are of the default 256 MiB f32 bench (MinMax and 1-bit)
     traffic = (pmc_traffic(names[dom], PMC_SUMMARY_ONEBIT if onebit else PMC_SUMMARY)
                if (args.dtype == "f32" and n == (1 << 26)) else None)
+    summary = PMC_SUMMARY_ONEBIT if onebit else PMC_SUMMARY
     roof = {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            # the PMC bytes are read from a committed rocprofv3 --pmc record of this command, not
+            # counted during this run (counters need their own profiler passes)
+            "traffic_source": (f"{os.path.relpath(summary, ROOT)} (committed rocprofv3 --pmc FETCH_SIZE / "
+                               "WRITE_SIZE passes of this bench command; not live)") if traffic else None,
             "alg_bytes_per_launch": alg[dom], "avg_launch_us": round(per[dom] * 1e3, 2),
             "compulsory_bytes_per_launch": compulsory[dom],
             "compulsory_frac": round(compulsory[dom] / (per[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
@@ -842,6 +847,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
 
     side_errors = {}
     skipped = []  # side lines not started because the line's wall budget was spent
+    side_steps = {}  # side lines timed over fewer steps than usual to fit the budget
 
     def remaining_s() -> float:
         # the line's wall budget left, the same on every rank (min over ranks, gloo), so
@@ -883,7 +889,16 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         timer.start()
         res = float("nan")
         try:
-            res = timed(fn, max(3, args.steps // 2), max(1, args.warmup // 2))
+            for _ in range(max(1, args.warmup // 2)):
+                fn()
+            # one timed call sizes the line: as many steps as fit in a fifth of what is left
+            # (t1 is the max over ranks and `left` the min, so every rank runs the same count)
+            nominal = max(3, args.steps // 2)
+            t1 = timed(fn, 1, 0)
+            steps = max(2, min(nominal, int(0.2 * max(0.0, left) / max(t1, 1e-9))))
+            if steps < nominal:
+                side_steps[name] = steps
+            res = timed(fn, steps, 0)
         except Exception as e:  # noqa: BLE001
             side_errors.setdefault(name, str(e)[:200])
         finally:
@@ -1139,6 +1154,8 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         extra["side_errors"] = side_errors
     extra["budget_s"] = args.budget_s
     extra["skipped_for_budget"] = skipped
+    if side_steps:
+        extra["side_steps_for_budget"] = side_steps
     if headline_fallback:
         extra["headline_fallback"] = headline_fallback
     del comm

@@ -58,6 +58,8 @@ def test_default_run_is_config2_with_cpu_baseline(default_line):
     assert abs(d["value"] - 256 / 1024 / (d["ms_per_step"] * 1e-3)) < 0.01 * d["value"]
     assert d["roofline"]["kernel"] == "minmax_resident_encode_kernel"
     assert d["roofline"]["traffic"] and d["roofline"]["traffic"] > 0  # committed PMC summary
+    src = d["roofline"]["traffic_source"]  # labelled as a committed record, not a live count
+    assert src.startswith("profiles/") and "not live" in src and os.path.exists(os.path.join(ROOT, src.split()[0]))
     check_cpu(d)
     # the CPU leg runs on the same 256 MiB bucket, and its bytes equal the GPU's
     assert "256 MiB bucket" in d["cpu_baseline"]["sample"] and d["cpu_baseline"]["matches_gpu_bytes"] is True
@@ -103,7 +105,11 @@ def test_default_line_carries_config4_point(default_line, allreduce_line):
     ks = a["op_kernels_us"]
     assert ks and all(v > 0 for v in ks.values())
     r = a["roofline"]
-    assert r and r["kernel"] in {k.split(":", 1)[1] for k in ks} and 0 < r["frac"] < 1.2
+    assert r and r["kernel"] in {k.split(":", 1)[1] for k in ks}
+    # algorithmic bytes above peak are possible only for the one-launch encode, whose SURVEY
+    # figure counts a second read it serves on chip; every other kernel's algorithmic bytes
+    # are its compulsory bytes, so a frac of 1 or more there would mean skipped work
+    assert 0 < r["frac"] < (1.2 if r["kernel"] == "minmax_resident_encode_kernel" else 1.0), r
     ref = allreduce_line["ms_per_step"]
     assert abs(a["ms_per_step"] - ref) <= 0.05 * ref, (a["ms_per_step"], ref)
     # and config 5 (2^27 bf16 ring op) at one rank
