@@ -106,6 +106,8 @@ KERNEL_SIGNATURES = {
     "bagua_minmax_u8_reduce_piece": (_i32, [_i32, _vp, _sz, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _sz, _vp]),
     "bagua_minmax_u8_requantize_pieces": (_i32, [_i32, _vp, _i32, _i32, _vp, _sz, _i32, _i32, _vp, _sz, _vp]),
     "bagua_minmax_u8_requantize_piece": (_i32, [_i32, _vp, _i32, _i32, _vp, _sz, _i32, _i32, _i32, _vp, _sz, _vp]),
+    "bagua_minmax_u8_reduce_requantize_piece": (_i32, [_i32, _vp, _sz, _i32, _i32, _i32, _vp, _sz, _i32, _i32, _i32,
+                                                        _vp, _sz, _vp]),
     "bagua_ring_mix_minmax": (_i32, [_i32, _vp, _vp, _vp, _vp, _i32, _vp, _sz, _vp]),
     "bagua_ring_apply_minmax": (_i32, [_i32, _vp, _vp, _vp, _sz, _i32, _vp, _vp, _vp, _vp, _vp]),
     "bagua_ring_apply_minmax_range": (_i32, [_i32, _vp, _vp, _vp, _sz, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),

@@ -625,7 +625,7 @@ int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void*
 template <typename T>
 int dequant_reduce_quantize_impl(const uint8_t* in, size_t in_bytes, int cs, int p, int average,
                                  const uint2* partials, int npartials, uint8_t* seg, int64_t seg_bytes, int blocks,
-                                 hipStream_t s, void* final_chunk);
+                                 hipStream_t s, void* final_chunk, int e0 = 0, int e1 = -1);
 
 template <typename T>
 static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, void* tensor, int average,
@@ -711,20 +711,53 @@ static int piece_blocks(int cs, int schedule, int per_vec) {
     return fused_blocks(longest, per_vec);
 }
 
+// tensor == nullptr: the piece's min/max partials only, nothing stored (the
+// requantise then recomputes the piece from the received segments:
+// reduce_requantize_piece_impl)
 template <typename T>
 static int reduce_piece_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, void* tensor, int average,
                              int target, int pieces, int piece, void* ws, size_t ws_bytes, hipStream_t s) {
     using S = typename T::storage;
-    if (p <= 0 || cs < 0 || target < 0 || target >= p || !tensor || !piece_schedule_ok(pieces) || piece < 0 ||
+    if (p <= 0 || cs < 0 || target < 0 || target >= p || !piece_schedule_ok(pieces) || piece < 0 ||
         piece >= piece_count(pieces))
         return BAGUA_ERR_INVALID_ARG;
     const int blocks = piece_blocks(cs, pieces, Vec<T>::N);
     if (!ws || ws_bytes < (size_t)piece_count(pieces) * blocks * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
     int b, e;
     piece_range(cs, pieces, piece, &b, &e);
-    S* chunk = static_cast<S*>(tensor) + (int64_t)target * cs;
+    S* chunk = tensor ? static_cast<S*>(tensor) + (int64_t)target * cs : nullptr;
     return dequant_reduce_impl<T>(recv, recv_bytes, cs, p, chunk, average,
                                   static_cast<uint2*>(ws) + (size_t)piece * blocks, blocks, s, b, e);
+}
+
+// Requantise piece `piece` of the own chunk straight from the p received segments:
+// fold every piece's partials (bagua_minmax_u8_reduce_piece with tensor == nullptr),
+// recompute the reduced values (the same tables and summation tree, so the same T
+// values bit for bit) and quantise them into segment `target` of `out` -- the bytes
+// reduce_piece (storing) + requantize_piece write, without storing the reduced chunk
+// and reading it back: (2p + 1) L bytes per piece of L elements instead of (p + 9) L
+// at fp32.
+template <typename T>
+static int reduce_requantize_piece_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, int average,
+                                        uint8_t* out, size_t out_bytes, int target, int pieces, int piece,
+                                        const void* ws, size_t ws_bytes, hipStream_t s) {
+    if (p <= 0 || cs < 0 || target < 0 || target >= p || !out || !piece_schedule_ok(pieces) || piece < 0 ||
+        piece >= piece_count(pieces))
+        return BAGUA_ERR_INVALID_ARG;
+    if (p > kMaxFusedChunks) return BAGUA_ERR_UNSUPPORTED;
+    const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);
+    if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
+    const int blocks = piece_blocks(cs, pieces, Vec<T>::N);
+    const int partials = piece_count(pieces) * blocks;
+    if (!ws || ws_bytes < (size_t)partials * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
+    int b, e;
+    piece_range(cs, pieces, piece, &b, &e);
+    if (b == e && piece > 0) return BAGUA_OK;  // empty trailing piece: its bytes were written by the others
+    const int grid = (int)std::min<int64_t>(fused_blocks(e - b, Vec<T>::N),
+                                            tune_int("BAGUA_TUNE_RRQ_BLOCKS", fold_grid_target(partials)));
+    return dequant_reduce_quantize_impl<T>(recv, recv_bytes, cs, p, average, static_cast<const uint2*>(ws), partials,
+                                           out + (int64_t)target * chunk_offset, chunk_offset, grid, s, nullptr, b,
+                                           e);
 }
 
 // requantise elements [e0, e1) of the own chunk from every piece's partials (the
@@ -970,6 +1003,16 @@ int bagua_minmax_u8_reduce_piece(int dtype, const uint8_t* input, size_t input_b
     hipStream_t s = static_cast<hipStream_t>(stream);
     BAGUA_DTYPE_DISPATCH(dtype, reduce_piece_impl<T>(input, input_bytes, chunk_size, num_chunks, tensor, average,
                                                      target_chunk, pieces, piece, workspace, workspace_bytes, s));
+}
+
+int bagua_minmax_u8_reduce_requantize_piece(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                                            int num_chunks, int average, uint8_t* output, size_t output_bytes,
+                                            int target_chunk, int pieces, int piece, const void* workspace,
+                                            size_t workspace_bytes, bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    BAGUA_DTYPE_DISPATCH(dtype, reduce_requantize_piece_impl<T>(input, input_bytes, chunk_size, num_chunks, average,
+                                                                output, output_bytes, target_chunk, pieces, piece,
+                                                                workspace, workspace_bytes, s));
 }
 
 int bagua_minmax_u8_requantize_pieces(int dtype, const void* tensor, int chunk_size, int num_chunks, uint8_t* output,

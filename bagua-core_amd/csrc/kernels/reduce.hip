@@ -330,10 +330,14 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
 // seg == nullptr, skip the segment (nothing reads it: one rank gathers nothing;
 // plain stores of it left 268 MB dirty in the Infinity Cache in front of the next
 // 1 GiB encode, +40 us, nt stores cost the kernel +76 us).
+//
+// A range [e0, e0 + cs) of the chunk (cs_total elements; the pipelined op's pieces):
+// the range at element 0 writes the header, the one ending at cs_total the slack.
 template <typename T, int BY, int AV, int PF = 0, bool FINAL = false>
 __global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
     const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int p, const uint2* __restrict__ partials,
-    int npartials, uint8_t* __restrict__ seg, int64_t seg_bytes, typename T::storage* __restrict__ final_out) {
+    int npartials, uint8_t* __restrict__ seg, int64_t seg_bytes, typename T::storage* __restrict__ final_out,
+    int64_t e0, int64_t cs_total) {
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
     __shared__ QParams qp[kMaxFusedChunks];
@@ -362,7 +366,7 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
     }
     if (blockIdx.x == 0 && (!FINAL || seg)) {
         const int t = threadIdx.x;
-        if (t < 32) {  // header {T min, T max, zero gap}
+        if (t < 32 && e0 == 0) {  // header {T min, T max, zero gap}
             const uint32_t bmn = sizeof(S) == 4 ? __float_as_uint(mn) : (uint32_t)T::from_f(mn);
             const uint32_t bmx = sizeof(S) == 4 ? __float_as_uint(mx) : (uint32_t)T::from_f(mx);
             uint32_t hb = 0;
@@ -370,11 +374,12 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
             else if (t < 2 * (int)sizeof(S)) hb = (bmx >> (8 * (t - (int)sizeof(S)))) & 0xff;
             seg[t] = (uint8_t)hb;
         }
-        for (int64_t j = 32 + cs + t; j < seg_bytes; j += kBlock) seg[j] = 0;  // slack
+        if (e0 + cs == cs_total)
+            for (int64_t j = 32 + cs_total + t; j < seg_bytes; j += kBlock) seg[j] = 0;  // slack
     }
-    uint8_t* payload = seg ? seg + 32 : nullptr;  // FINAL without a segment writes no payload
+    uint8_t* payload = seg ? seg + 32 + e0 : nullptr;  // FINAL without a segment writes no payload
     reduce_tiles<T, BY, AV, PF>(
-        in + 32, chunk_offset, cs, p, lut,
+        in + 32 + e0, chunk_offset, cs, p, lut,
         [&](int64_t v, const uint4& packed) {
             float st[N];
             unpack16<T>(packed, st);
@@ -434,44 +439,49 @@ static void dispatch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs
     }
 }
 
+// range [e0, e0 + len) of a chunk of cs elements
+struct RqRange {
+    int64_t e0, len, cs;
+};
+
 template <typename T, int AV, int PF, bool FINAL>
-static void launch_reduce_quantize(int by, const uint8_t* in, int64_t co, int64_t cs, int p, const uint2* partials,
+static void launch_reduce_quantize(int by, const uint8_t* in, int64_t co, RqRange r, int p, const uint2* partials,
                                    int npartials, uint8_t* seg, int64_t seg_bytes, typename T::storage* final_out,
                                    int blocks, hipStream_t s) {
     switch (by) {
         case 2:
             launch((dequant_reduce_quantize_kernel<T, 2, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                   cs, p, partials, npartials, seg, seg_bytes, final_out);
+                   r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs);
             break;
         case 4:
             launch((dequant_reduce_quantize_kernel<T, 4, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                   cs, p, partials, npartials, seg, seg_bytes, final_out);
+                   r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs);
             break;
         default:
             launch((dequant_reduce_quantize_kernel<T, 8, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                   cs, p, partials, npartials, seg, seg_bytes, final_out);
+                   r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs);
             break;
     }
 }
 
 template <typename T, int AV>
-static void dispatch_reduce_quantize(const uint8_t* in, int64_t co, int64_t cs, int p, const uint2* partials,
+static void dispatch_reduce_quantize(const uint8_t* in, int64_t co, RqRange r, int p, const uint2* partials,
                                      int npartials, uint8_t* seg, int64_t seg_bytes, typename T::storage* final_out,
                                      int blocks, hipStream_t s) {
     if (p == 1) {  // one segment: the BY = 2 tree with p known (no duplicate loads)
         if (final_out)
-            launch_reduce_quantize<T, AV, 1, true>(2, in, co, cs, p, partials, npartials, seg, seg_bytes, final_out,
+            launch_reduce_quantize<T, AV, 1, true>(2, in, co, r, p, partials, npartials, seg, seg_bytes, final_out,
                                                    blocks, s);
         else
-            launch_reduce_quantize<T, AV, 1, false>(2, in, co, cs, p, partials, npartials, seg, seg_bytes, nullptr,
+            launch_reduce_quantize<T, AV, 1, false>(2, in, co, r, p, partials, npartials, seg, seg_bytes, nullptr,
                                                     blocks, s);
         return;
     }
     if (final_out)
-        launch_reduce_quantize<T, AV, 0, true>(reduce_by(p), in, co, cs, p, partials, npartials, seg, seg_bytes,
+        launch_reduce_quantize<T, AV, 0, true>(reduce_by(p), in, co, r, p, partials, npartials, seg, seg_bytes,
                                                final_out, blocks, s);
     else
-        launch_reduce_quantize<T, AV, 0, false>(reduce_by(p), in, co, cs, p, partials, npartials, seg, seg_bytes,
+        launch_reduce_quantize<T, AV, 0, false>(reduce_by(p), in, co, r, p, partials, npartials, seg, seg_bytes,
                                                 nullptr, blocks, s);
 }
 
@@ -506,25 +516,30 @@ int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void*
 
 // quantise the reduced chunk, recomputed from the p received segments, into `seg`
 // (seg_bytes: the segment incl. header and slack), after dequant_reduce_impl with
-// out == nullptr emitted `npartials` partials (the same `blocks`)
+// out == nullptr emitted `npartials` partials; `blocks` is this launch's grid.
+// Elements [e0, e1) only (default: the whole chunk); final_chunk needs the whole chunk.
 template <typename T>
 int dequant_reduce_quantize_impl(const uint8_t* in, size_t in_bytes, int cs, int p, int average,
                                  const uint2* partials, int npartials, uint8_t* seg, int64_t seg_bytes, int blocks,
-                                 hipStream_t s, void* final_chunk) {
+                                 hipStream_t s, void* final_chunk, int e0, int e1) {
     using S = typename T::storage;
-    if (!in || !partials || (!seg && !final_chunk) || cs < 0 || p <= 0 || npartials < 1) return BAGUA_ERR_INVALID_ARG;
+    if (e1 < 0) e1 = cs;
+    if (!in || !partials || (!seg && !final_chunk) || cs < 0 || p <= 0 || npartials < 1 || e0 < 0 || e1 < e0 ||
+        e1 > cs || (final_chunk && (e0 != 0 || e1 != cs)))
+        return BAGUA_ERR_INVALID_ARG;
     if (p > kMaxFusedChunks) return BAGUA_ERR_UNSUPPORTED;
     const int64_t co = (int64_t)(in_bytes / (size_t)p);
     if (co < (int64_t)cs + 32 || (seg && seg_bytes < (int64_t)cs + 32)) return BAGUA_ERR_INVALID_ARG;
     constexpr int N = Vec<T>::N;
-    const bool aligned = (((uintptr_t)in + 32) % N == 0) && (co % N == 0) && (((uintptr_t)seg + 32) % N == 0) &&
-                         ((uintptr_t)final_chunk % 16 == 0);
+    const bool aligned = (((uintptr_t)in + 32 + e0) % N == 0) && (co % N == 0) &&
+                         (((uintptr_t)seg + 32 + e0) % N == 0) && ((uintptr_t)final_chunk % 16 == 0);
     if (!aligned) return BAGUA_ERR_UNSUPPORTED;
     S* const fo = static_cast<S*>(final_chunk);
+    const RqRange r{e0, (int64_t)e1 - e0, cs};
     switch (avg_mode(average, p)) {
-        case 0: dispatch_reduce_quantize<T, 0>(in, co, cs, p, partials, npartials, seg, seg_bytes, fo, blocks, s); break;
-        case 1: dispatch_reduce_quantize<T, 1>(in, co, cs, p, partials, npartials, seg, seg_bytes, fo, blocks, s); break;
-        default: dispatch_reduce_quantize<T, 2>(in, co, cs, p, partials, npartials, seg, seg_bytes, fo, blocks, s); break;
+        case 0: dispatch_reduce_quantize<T, 0>(in, co, r, p, partials, npartials, seg, seg_bytes, fo, blocks, s); break;
+        case 1: dispatch_reduce_quantize<T, 1>(in, co, r, p, partials, npartials, seg, seg_bytes, fo, blocks, s); break;
+        default: dispatch_reduce_quantize<T, 2>(in, co, r, p, partials, npartials, seg, seg_bytes, fo, blocks, s); break;
     }
     return check_launch();
 }
@@ -533,11 +548,11 @@ template int dequant_reduce_impl<F32>(const uint8_t*, size_t, int, int, void*, i
 template int dequant_reduce_impl<F16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
 template int dequant_reduce_impl<BF16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
 template int dequant_reduce_quantize_impl<F32>(const uint8_t*, size_t, int, int, int, const uint2*, int, uint8_t*,
-                                               int64_t, int, hipStream_t, void*);
+                                               int64_t, int, hipStream_t, void*, int, int);
 template int dequant_reduce_quantize_impl<F16>(const uint8_t*, size_t, int, int, int, const uint2*, int, uint8_t*,
-                                               int64_t, int, hipStream_t, void*);
+                                               int64_t, int, hipStream_t, void*, int, int);
 template int dequant_reduce_quantize_impl<BF16>(const uint8_t*, size_t, int, int, int, const uint2*, int, uint8_t*,
-                                                int64_t, int, hipStream_t, void*);
+                                                int64_t, int, hipStream_t, void*, int, int);
 
 }  // namespace bagua
 

@@ -561,15 +561,26 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
         TRY2(exchange_piece(c, k, sb, rb, lo, hi, true));
         HIP2(hipEventRecord(exchanged[q], s1));
     }
-    // 2. reduce the p received versions of the own chunk piece by piece, requantise it
+    // 2. reduce the p received versions of the own chunk piece by piece, requantise it.
+    // By default the reduced chunk is not stored: each reduce piece emits its min/max
+    // partials only and the requantise recomputes the piece from the received segments
+    // ((2p + 1) L bytes per piece instead of (p + 9) L at fp32; the own chunk of x is
+    // rewritten by the final dequantise anyway).  BAGUA_PIPE_RECOMPUTE=0: the storing
+    // pair (A/B).
+    const bool recompute = env_int("BAGUA_PIPE_RECOMPUTE", 1) != 0;
     for (int q = 0; q < pieces; ++q) {
         HIP2(hipStreamWaitEvent(s0, exchanged[q], 0));
-        TRY2(bagua_minmax_u8_reduce_piece(dt, rb, k.S, cs, p, x, average, k.rank, sched, q, ws, ws_bytes, s0));
+        TRY2(bagua_minmax_u8_reduce_piece(dt, rb, k.S, cs, p, recompute ? nullptr : x, average, k.rank, sched, q, ws,
+                                          ws_bytes, s0));
     }
     // requantise piece by piece (each folds every piece's partials), so the allgather of
     // piece q starts while piece q+1 is requantised
     for (int q = 0; q < pieces; ++q) {
-        TRY2(bagua_minmax_u8_requantize_piece(dt, x, cs, p, sb, k.S, k.rank, sched, q, ws, ws_bytes, s0));
+        if (recompute)
+            TRY2(bagua_minmax_u8_reduce_requantize_piece(dt, rb, k.S, cs, p, average, sb, k.S, k.rank, sched, q, ws,
+                                                         ws_bytes, s0));
+        else
+            TRY2(bagua_minmax_u8_requantize_piece(dt, x, cs, p, sb, k.S, k.rank, sched, q, ws, ws_bytes, s0));
         HIP2(hipEventRecord(requantised_piece[q], s0));
     }
     // 3. allgather + dequantise piece by piece

@@ -478,7 +478,7 @@ def bench_host(args):
     def h2d(b):
         # the copies go in `chunks` pieces: one 256 MiB H2D next to one D2H sometimes
         # does not overlap at all (9.4 ms for the pair vs 4.7 ms each), two pieces per
-        # copy overlap every time (5.6 ms; bagua-core_amd/tools/pcie_probe.py,
+        # copy overlap every time (5.6 ms; tools/pcie_probe.py,
         # profiles/r02_host_copy_ab.jsonl)
         step = (n + chunks - 1) // chunks
         for lo in range(0, n, step):

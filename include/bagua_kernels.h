@@ -261,6 +261,19 @@ int bagua_minmax_u8_requantize_pieces(int dtype, const void* tensor, int chunk_s
 int bagua_minmax_u8_requantize_piece(int dtype, const void* tensor, int chunk_size, int num_chunks, uint8_t* output,
                                      size_t output_bytes, int target_chunk, int pieces, int piece,
                                      const void* workspace, size_t workspace_bytes, bagua_stream_t stream);
+/* The same pipeline without storing the reduced chunk: bagua_minmax_u8_reduce_piece
+ * with tensor == NULL emits each piece's min/max partials only, and
+ * bagua_minmax_u8_reduce_requantize_piece recomputes piece `piece` of the reduced
+ * target chunk from the p received segments (`input`, as reduce_piece read them:
+ * same tables, same summation tree, so the same values bit for bit), folds every
+ * piece's partials and quantises it into segment target_chunk of `output` (the
+ * range at 0 writes the header, the one ending at chunk_size the slack).  The
+ * tensor is left untouched.  BAGUA_ERR_UNSUPPORTED for num_chunks > 16 or
+ * misaligned segments (use the storing pair). */
+int bagua_minmax_u8_reduce_requantize_piece(int dtype, const uint8_t* input, size_t input_bytes, int chunk_size,
+                                            int num_chunks, int average, uint8_t* output, size_t output_bytes,
+                                            int target_chunk, int pieces, int piece, const void* workspace,
+                                            size_t workspace_bytes, bagua_stream_t stream);
 
 /* Decentralized ring op (decentralized_low_precision_synchronous.rs:45-64,126-151)
  * as two fused passes around the MinMax quantise pass, bit-identical to the

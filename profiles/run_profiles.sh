@@ -36,7 +36,7 @@ step trace_ar1 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT
   python3 bench.py --workload allreduce --steps 20 --warmup 3 --no-cpu-baseline --no-decentralized \
   > "$OUT/ar1_under_rocprof.json"
 step ring_trace 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ring_trace" -o ring -- \
-  python3 bagua-core_amd/tools/ring_probe.py --steps 10
+  python3 tools/ring_probe.py --steps 10
 step b_codec 200 python3 bench.py > "$OUT/b_codec.json"
 step b_onebit 200 python3 bench.py --workload onebit > "$OUT/b_onebit.json"
 step b_bf16 200 python3 bench.py --dtype bf16 > "$OUT/b_codec_bf16.json"

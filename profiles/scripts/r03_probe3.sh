@@ -12,6 +12,6 @@ step() {
   local rc=$?
   if [ $rc -ne 0 ]; then echo "[r03] $name failed rc=$rc" >&2; exit $rc; fi
 }
-step apply_sweep 500 python3 bagua-core_amd/tools/ring_apply_sweep.py --cfgs 0,14,16,17,18,19,20,21,22 --rounds 4 \
+step apply_sweep 500 python3 tools/ring_apply_sweep.py --cfgs 0,14,16,17,18,19,20,21,22 --rounds 4 \
   > "$O/ring_apply_sweep3.jsonl"
 echo "[r03] done" >&2

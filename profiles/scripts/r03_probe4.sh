@@ -11,7 +11,7 @@ step() {
   local rc=$?
   if [ $rc -ne 0 ]; then echo "[r03] $name failed rc=$rc" >&2; exit $rc; fi
 }
-step grid_sweep 400 python3 bagua-core_amd/tools/grid_sweep.py --rounds 4 --steps 30 > "$O/grid_sweep.jsonl"
+step grid_sweep 400 python3 tools/grid_sweep.py --rounds 4 --steps 30 > "$O/grid_sweep.jsonl"
 step ring_tests 400 python3 -u -m pytest tests/test_gpu_multirank.py tests/test_gpu_fullsize.py -k "decentralized" -x -q \
   --timeout 120 --timeout-method thread
 echo "[r03] done" >&2

@@ -15,5 +15,5 @@ step comm_tests 500 python3 -u -m pytest tests/test_gpu_comm.py tests/test_gpu_b
   tests/test_gpu_c_abi.py tests/test_gpu_bench.py -x -q --timeout 200 --timeout-method thread
 step b_ar1 300 python3 bench.py --workload allreduce > "$O/b_ar1_v2.json"
 step b_backend 300 python3 bench.py --workload backend --steps 10 > "$O/b_backend_v2.json"
-step ring 120 python3 bagua-core_amd/tools/ring_probe.py --steps 20
+step ring 120 python3 tools/ring_probe.py --steps 20
 echo "[r03] done" >&2

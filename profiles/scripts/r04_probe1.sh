@@ -6,7 +6,7 @@ set -u
 OUT=gpurun_out/r04p1
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-T=bagua-core_amd/tools
+T=tools
 step() {  # name timeout cmd...: stop at the first failure (fault, abort, time limit)
   local name=$1 to=$2; shift 2
   echo "[probe] $name $(date +%T)" >&2

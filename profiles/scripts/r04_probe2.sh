@@ -6,7 +6,7 @@ set -u
 OUT=gpurun_out/r04p2
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-T=bagua-core_amd/tools
+T=tools
 step() {
   local name=$1 to=$2; shift 2
   echo "[probe2] $name $(date +%T)" >&2

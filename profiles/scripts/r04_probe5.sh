@@ -4,7 +4,7 @@
 set -u
 OUT=gpurun_out/r04p5
 mkdir -p "$OUT"
-T=bagua-core_amd/tools
+T=tools
 step() {
   local name=$1 to=$2; shift 2
   echo "[probe5] $name $(date +%T)" >&2

@@ -5,7 +5,7 @@
 set -u
 OUT=gpurun_out/r04p8
 mkdir -p "$OUT"
-T=bagua-core_amd/tools
+T=tools
 step() {
   local name=$1 to=$2; shift 2
   echo "[probe8] $name $(date +%T)" >&2

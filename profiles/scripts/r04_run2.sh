@@ -6,4 +6,4 @@ echo "pytest rc=$rc" >> gpurun_out/r04_gputests2.log
 # a test failure (rc 1) still lets the bench run; a crash, abort or time limit ends the call
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 240 python -u bench.py > gpurun_out/r04_bench_default2.json 2> gpurun_out/r04_bench_default2.err && \
-bash bagua-core_amd/tools/r04_sched.sh > gpurun_out/r04_sched.log 2>&1
+bash tools/r04_sched.sh > gpurun_out/r04_sched.log 2>&1

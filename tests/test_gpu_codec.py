@@ -261,8 +261,26 @@ def test_fused_reduce_requantize(bc, oracle_c, dtype, p, ragged, mode, average):
     assert np.all(got[other] == 0xA5), "bytes outside the target segment written"
 
 
-@pytest.mark.parametrize("dtype", [F32, BF16])
-@pytest.mark.parametrize("p,pieces", [(1, 3), (2, 4), (4, 2), (8, 5)])
+def recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces, ws, send_want, t_untouched=False):
+    """bagua_minmax_u8_reduce_piece(tensor = NULL) per piece, then
+    bagua_minmax_u8_reduce_requantize_piece per piece (reverse order): segment r equals the
+    oracle's decompress + reduce_mean + compress(target), no other byte is written."""
+    co = S // p
+    send_d = torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
+    n = pieces & 0xFFFF
+    for q in range(n):
+        assert K.bagua_minmax_u8_reduce_piece(dtype, recv_d.data_ptr(), S, cs, p, None, 1, r, pieces, q,
+                                              ws.data_ptr(), ws.numel(), None) == 0
+    for q in reversed(range(n)):
+        assert K.bagua_minmax_u8_reduce_requantize_piece(dtype, recv_d.data_ptr(), S, cs, p, 1, send_d.data_ptr(), S,
+                                                         r, pieces, q, ws.data_ptr(), ws.numel(), None) == 0
+    got = send_d.cpu().numpy()
+    assert np.array_equal(got[r * co:(r + 1) * co], send_want[r * co:(r + 1) * co]), (p, pieces)
+    assert np.all(np.delete(got, np.s_[r * co:(r + 1) * co]) == 0xA5)
+
+
+@pytest.mark.parametrize("dtype", [F32, F16, BF16])
+@pytest.mark.parametrize("p,pieces", [(1, 3), (2, 4), (4, 2), (8, 5), (3, 3), (16, 4)])
 def test_minmax_piecewise_building_blocks(bc, oracle_c, dtype, p, pieces):
     """The pipelined op's MinMax building blocks reproduce the unpieced bytes: quantize_range over
     every piece (after the stage-1 partials) == compress; reduce_piece + requantize_piece over every
@@ -310,6 +328,11 @@ def test_minmax_piecewise_building_blocks(bc, oracle_c, dtype, p, pieces):
     got = send_d.cpu().numpy()
     assert np.array_equal(got[r * co:(r + 1) * co], send_want[r * co:(r + 1) * co])
     assert np.all(np.delete(got, np.s_[r * co:(r + 1) * co]) == 0xA5)
+    # 2b. the op's default middle step: partials-only reduce pieces, then every piece
+    # requantised straight from the received segments (tensor untouched), same bytes
+    recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces, ws, send_want, t_untouched=True)
+    if pieces >= 3:  # the tapered schedule (first and last piece half size)
+        recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces | bc._native.PIECES_TAPERED, ws, send_want)
     # 3. decompress, piece by piece
     y_d = torch.zeros(p * cs, dtype=TORCH[dtype], device="cuda")
     for q in range(pieces):

@@ -14,7 +14,7 @@ Algorithmic bytes per launch (SURVEY §8(d), N fp32 elements, p = 1):
   minmax_partials 4N, minmax_quantize 5N + 32, minmax_dequantize 5N + 32,
   onebit_encode 4N + N/8 (+ tile partials), onebit_decode N/8 + 4N.
 
-  python bagua-core_amd/tools/cache_state_probe.py [--reps 7] [--out file.jsonl]
+  python tools/cache_state_probe.py [--reps 7] [--out file.jsonl]
 """
 import argparse
 import ctypes
@@ -25,7 +25,7 @@ import sys
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "bagua-core_amd"))
 
 from bagua_core import _native as N  # noqa: E402
 

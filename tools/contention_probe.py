@@ -2,7 +2,7 @@
 compute-bound kernel stream runs beside it, as in Bagua, where the comm ops
 overlap the backward pass (DESIGN.md §5.1 "Under contention").
 
-  python bagua-core_amd/tools/contention_probe.py [--gemm 8192] [--modes resident,two_pass]
+  python tools/contention_probe.py [--gemm 8192] [--modes resident,two_pass]
 
 Per encode mode (the one-launch encode, or BAGUA_RESIDENT=0's two kernels):
   alone       : codec steps on stream A only
@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "bagua-core_amd"))
 
 from bagua_core import _native as N  # noqa: E402
 

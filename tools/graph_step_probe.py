@@ -3,7 +3,7 @@
 launched eagerly vs replayed from a HIP graph (both kernels captured once),
 wall time per step over the same number of steps, interleaved.
 
-    python bagua-core_amd/tools/graph_step_probe.py [--steps 200]
+    python tools/graph_step_probe.py [--steps 200]
 """
 import argparse
 import ctypes
@@ -14,7 +14,7 @@ import time
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "bagua-core_amd"))
 
 

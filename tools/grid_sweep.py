@@ -5,7 +5,7 @@ call; launch_util.hpp tune_int).  A grid-strided kernel with a few workgroups
 per CU vs one tile per workgroup (the hardware dispatcher then balances the
 tail; the ring apply pass gained 20 % that way, profiles/r03_ring_apply_sweep3.jsonl).
 
-  python bagua-core_amd/tools/grid_sweep.py [--rounds 4 --steps 30]
+  python tools/grid_sweep.py [--rounds 4 --steps 30]
 
 Every variant's compressed bytes and decoded floats must equal the first
 variant's of its workload.  One JSON line per (round, variant), then summaries.
@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "bagua-core_amd"))
 
 from bagua_core import _native as N  # noqa: E402
 

@@ -3,7 +3,7 @@ timed loop, the GPU works behind): where the per-bucket host time of the
 scheduler workload goes (profiles/r03_backend_trace_summary.json shows the GPU
 idle 12-15 us between 25 MiB buckets).
 
-  python bagua-core_amd/tools/host_overhead_probe.py [--elements N]
+  python tools/host_overhead_probe.py [--elements N]
 
 Prints one JSON line: host us per call of each entry point (median of batches),
 and the GPU time per call for comparison.
@@ -19,7 +19,7 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "bagua-core_amd"))
 
 import bagua_core  # noqa: E402
 from bagua_core import _native as N  # noqa: E402

@@ -8,7 +8,7 @@ library's own kernel-recorded events (bagua_time_next_kernel: hipExtLaunchKernel
 / stop events around exactly that launch), and every workload's output bytes are
 compared between A and B (a speed change must not move a byte).
 
-  python3 bagua-core_amd/tools/kernel_ab.py [--base ab_libs/base/libbagua_kernels.so]
+  python3 tools/kernel_ab.py [--base ab_libs/base/libbagua_kernels.so]
         [--rounds 4] [--reps 10] [--only quant_bf16_ring,one_rank_1g]
 
 Prints one JSON object: per workload, A and B median us per launch and the
@@ -26,8 +26,8 @@ import sys
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-ROOT = os.path.dirname(os.path.dirname(HERE))
-sys.path.insert(0, os.path.dirname(HERE))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "bagua-core_amd"))
 
 from bagua_core import _native as N  # noqa: E402  (signatures of the in-tree build)
 

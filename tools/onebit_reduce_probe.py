@@ -5,7 +5,7 @@ chunk, reduce them in the reference's tree order, re-encode; + its finalize),
 timed with HIP events on one GPU for p = 1..16 chunks of a 1 GiB fp32 (or
 512 MiB bf16) bucket.  Prints the re-encoded segment's hash for A/B runs.
 
-    python bagua-core_amd/tools/onebit_reduce_probe.py [--dtype f32|bf16]
+    python tools/onebit_reduce_probe.py [--dtype f32|bf16]
 """
 import argparse
 import ctypes
@@ -16,7 +16,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "bagua-core_amd"))
 
 

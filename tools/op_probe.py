@@ -7,7 +7,7 @@ bytes to the op's building blocks as the op itself runs them (not standalone).
   transport (one host thread each, one GPU; their kernels overlap in time, so use
   p > 1 for counters, p = 1 for durations).
 
-  python bagua-core_amd/tools/op_probe.py --ranks 8 --method minmax --pieces 4 \
+  python tools/op_probe.py --ranks 8 --method minmax --pieces 4 \
       [--elements 268435456] [--iters 3] [--json out.json]
 
 The JSON lists, for rank 0's last op, every kernel in launch order with its
@@ -23,7 +23,7 @@ import threading
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "bagua-core_amd"))
 
 import bagua_core  # noqa: E402
 from bagua_core import _native as N  # noqa: E402

@@ -7,7 +7,7 @@ quantise of piece 0), the middle between the last alltoall and the first allgath
 piece (reduce of the last piece + requantise of piece 0), the suffix after the last
 allgather piece (dequantise of the last piece), and the total codec time per op.
 
-    python bagua-core_amd/tools/pipeline_kernels_probe.py [--pieces 4] [--reps 5]
+    python tools/pipeline_kernels_probe.py [--pieces 4] [--reps 5]
 """
 import argparse
 import ctypes
@@ -17,7 +17,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "bagua-core_amd"))
 
 
@@ -68,28 +68,62 @@ def main():
                                                                                 sp))
         q_us = [timed(lambda q=q: K.bagua_minmax_u8_quantize_range(0, xp, n, cs, p, cp, S, wp, wsb, -1, *rng(q), sp))
                 for q in range(P)]
-        # the received buffer: this rank's own compressed bytes stand in for the peers'
-        r_us = [timed(lambda q=q: K.bagua_minmax_u8_reduce_piece(0, cp, S, cs, p, xp, 1, r, P, q, wp, wsb, sp))
+        # the received buffer: a second copy of this rank's compressed bytes stands in for the
+        # peers' (its own segments differ from the ones it sends, as on a node)
+        recv = send.clone()
+        rp = recv.data_ptr()
+        # storing pair (BAGUA_PIPE_RECOMPUTE=0): the reduce piece stores the reduced piece of
+        # the own chunk (4 B per element) and the requantise reads it back
+        r_us = [timed(lambda q=q: K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp, 1, r, P, q, wp, wsb, sp))
                 for q in range(P)]
         rq_us = [timed(lambda q=q: K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, P, q, wp, wsb, sp))
                  for q in range(P)]
+        # the op's default: partials-only reduce pieces, the requantise recomputes from recv
+        r2_us = [timed(lambda q=q: K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, None, 1, r, P, q, wp, wsb, sp))
+                 for q in range(P)]
+        rq2_us = [timed(lambda q=q: K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, P, q, wp,
+                                                                              wsb, sp))
+                  for q in range(P)]
         d_us = [timed(lambda q=q: K.bagua_minmax_u8_decompress_range(0, cp, S, cs, p, xp, *rng(q), sp))
                 for q in range(P)]
-        row.update({"quantise_piece_us": [round(v, 1) for v in q_us], "reduce_piece_us": [round(v, 1) for v in r_us],
-                    "requantise_piece_us": [round(v, 1) for v in rq_us],
-                    "dequantise_piece_us": [round(v, 1) for v in d_us]})
+        r1 = lambda v: [round(u, 1) for u in v]
+        row.update({"quantise_piece_us": r1(q_us), "dequantise_piece_us": r1(d_us),
+                    "store": {"reduce_piece_us": r1(r_us), "requantise_piece_us": r1(rq_us)},
+                    "recompute": {"reduce_piece_us": r1(r2_us), "requantise_piece_us": r1(rq2_us)}})
         # algorithmic bytes per launch: piece q covers L_q elements of every chunk
         L = [rng(q)[1] - rng(q)[0] for q in range(P)]
         rate = lambda byts, us: round(byts / us / 1e3, 1)  # GB/s
         row["minmax_pass_gb_s"] = rate(4 * n, row["minmax_pass_us"])              # x read once
         row["quantise_piece_gb_s"] = [rate(5 * p * L[q], q_us[q]) for q in range(P)]  # x read, payload written
-        row["reduce_piece_gb_s"] = [rate(p * L[q], r_us[q]) for q in range(P)]        # p received payloads read
-        row["requantise_piece_gb_s"] = [rate((p + 1) * L[q], rq_us[q]) for q in range(P)]  # p read + own written
         row["dequantise_piece_gb_s"] = [rate(5 * p * L[q], d_us[q]) for q in range(P)]  # p payloads read, x written
+        # storing pair: reduce = p payloads read + the fp32 piece written; requantise = that piece
+        # read back + its payload written
+        row["store"]["reduce_piece_gb_s"] = [rate((p + 4) * L[q], r_us[q]) for q in range(P)]
+        row["store"]["requantise_piece_gb_s"] = [rate(5 * L[q], rq_us[q]) for q in range(P)]
+        # recompute: reduce = p payloads read; requantise = p payloads read + its payload written
+        row["recompute"]["reduce_piece_gb_s"] = [rate(p * L[q], r2_us[q]) for q in range(P)]
+        row["recompute"]["requantise_piece_gb_s"] = [rate((p + 1) * L[q], rq2_us[q]) for q in range(P)]
         row["prefix_us"] = round(row["minmax_pass_us"] + q_us[0], 1)
-        row["middle_us"] = round(r_us[-1] + rq_us[0], 1)
+        row["store"]["middle_us"] = round(r_us[-1] + rq_us[0], 1)
+        row["recompute"]["middle_us"] = round(r2_us[-1] + rq2_us[0], 1)
         row["suffix_us"] = round(d_us[-1], 1)
-        row["codec_total_us"] = round(row["minmax_pass_us"] + sum(q_us) + sum(r_us) + sum(rq_us) + sum(d_us), 1)
+        common = row["minmax_pass_us"] + sum(q_us) + sum(d_us)
+        row["store"]["codec_total_us"] = round(common + sum(r_us) + sum(rq_us), 1)
+        row["recompute"]["codec_total_us"] = round(common + sum(r2_us) + sum(rq2_us), 1)
+        # the recompute requantise writes the same bytes as the storing pair
+        K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp, 1, r, P, 0, wp, wsb, sp)
+        for q in range(P):
+            K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp, 1, r, P, q, wp, wsb, sp)
+        for q in range(P):
+            K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, P, q, wp, wsb, sp)
+        a = send.clone()
+        for q in range(P):
+            K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, None, 1, r, P, q, wp, wsb, sp)
+        for q in range(P):
+            K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, P, q, wp, wsb, sp)
+        torch.cuda.synchronize()
+        row["recompute_bytes_equal"] = bool(torch.equal(a, send))
+        del recv
         row["minmax_pass_us"] = round(row["minmax_pass_us"], 1)
         out[f"p{p}"] = row
         del send, ws

@@ -3,7 +3,7 @@ after another kernel's min/max partials: the config-5 ring op (bf16, partials
 from ring_mix_kernel) and the two-pass f32 encode (partials from
 minmax_partials_kernel).  BAGUA_TUNE_QUANT_BLOCKS per call; bytes must not change.
 
-  python bagua-core_amd/tools/quant_sweep.py [--rounds 4 --steps 20]
+  python tools/quant_sweep.py [--rounds 4 --steps 20]
 """
 import argparse
 import ctypes
@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "bagua-core_amd"))
 
 from bagua_core import _native as N  # noqa: E402
 

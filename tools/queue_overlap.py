@@ -3,7 +3,7 @@ which hardware queues the RCCL kernels and the codec kernels ran on, and how
 much of the codec kernels' time ran while an RCCL kernel of the same process
 was running (beside it, on another queue) versus after one ended.
 
-  python3 bagua-core_amd/tools/queue_overlap.py gpurun_out/q4 [label]
+  python3 tools/queue_overlap.py gpurun_out/q4 [label]
 
 Prints one JSON line: per rank, {queues used by each kind, codec busy time,
 codec time overlapped with RCCL kernels, fraction, the number of codec kernels

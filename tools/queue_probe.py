@@ -9,8 +9,8 @@ kernels on the op's stream run BESIDE them (separate hardware queues) or only
 after them (one queue, in order).  Start each rank under its own profiler:
 
   for r in 0 1; do GPU_MAX_HW_QUEUES=4 rocprofv3 --kernel-trace --output-format csv \
-      -d gpurun_out/q4/rank$r -o run -- python3 bagua-core_amd/tools/queue_probe.py $r 2 /tmp/qp & done; wait
-  python3 bagua-core_amd/tools/queue_overlap.py gpurun_out/q4
+      -d gpurun_out/q4/rank$r -o run -- python3 tools/queue_probe.py $r 2 /tmp/qp & done; wait
+  python3 tools/queue_overlap.py gpurun_out/q4
 
 Prints one JSON line per rank (the op's ms per step, the queue setting).
 """
@@ -28,7 +28,7 @@ os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
 os.environ.setdefault("NCCL_IB_DISABLE", "1")
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "bagua-core_amd"))
 
 import torch  # noqa: E402
 

@@ -1,6 +1,6 @@
 """Exhaustive check behind reduce.hip avg_finish: for p = 2, 4, 8, 16 and every f32 bit pattern,
 x * (1/p) == x / p bit for bit (NaN payloads aside).  ~1 min on the CPU:
-    python bagua-core_amd/tools/recip_exact_check.py
+    python tools/recip_exact_check.py
 """
 import numpy as np, sys
 bad = 0

@@ -3,7 +3,7 @@
 the compressed all-reduce) and the dequantise kernel, timed with HIP events on
 one GPU for p = 2..16 chunks of a 1 GiB fp32 (or 512 MiB bf16) bucket.
 
-    python bagua-core_amd/tools/reduce_probe.py [--lib path/to/libbagua_kernels.so] [--dtype f32|bf16]
+    python tools/reduce_probe.py [--lib path/to/libbagua_kernels.so] [--dtype f32|bf16]
 
 `--lib` times another build of the kernel library INSTEAD of the in-tree one
 (loaded with RTLD_DEEPBIND so its internal calls stay inside it; run the two
@@ -18,7 +18,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "bagua-core_amd"))
 
 

@@ -3,7 +3,7 @@ MinMax-UInt8 encode + decode), in ONE process on one box: every library is
 loaded side by side (ctypes, RTLD_LOCAL, by path), and rounds alternate the
 order, so box and clock drift hit every build alike.
 
-  python bagua-core_amd/tools/resident_ab.py --lib r01=ab_libs/r01/libbagua_kernels.so \
+  python tools/resident_ab.py --lib r01=ab_libs/r01/libbagua_kernels.so \
       --lib head=bagua-core_amd/lib/libbagua_kernels.so [--rounds 8 --steps 40]
 
 Per build: every encode and decode launch is timed by the kernel's own HIP

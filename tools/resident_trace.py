@@ -2,7 +2,7 @@
 kernel configuration, from the kernel's own wall_clock64 stamps
 (bagua_minmax_u8_resident_trace): pass 1, exchange, pass 2, per workgroup.
 
-  python bagua-core_amd/tools/resident_trace.py [--elements N] [--cfgs 0,1,2]
+  python tools/resident_trace.py [--elements N] [--cfgs 0,1,2]
 
 Prints one JSON line per configuration (medians over workgroups and runs, us).
 """
@@ -16,7 +16,7 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "bagua-core_amd"))
 
 from bagua_core import _native as N  # noqa: E402
 

@@ -2,7 +2,7 @@
 BAGUA_RING_APPLY_CFG) on 2^27 bf16 elements: store policy per output, nt loads,
 contiguous ranges, unroll, grid size.
 
-  python bagua-core_amd/tools/ring_apply_sweep.py [--cfgs 0,1,2,...] [--rounds 4]
+  python tools/ring_apply_sweep.py [--cfgs 0,1,2,...] [--rounds 4]
 
 1. every variant's four outputs must equal variant 0's bit for bit (one apply
    from the same saved state);
@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "bagua-core_amd"))
 
 import bagua_core  # noqa: E402
 from bagua_core import _native as N  # noqa: E402

@@ -14,7 +14,7 @@ Algorithmic bytes per launch, N elements of T (sizeof 2), the MinMax payload N +
   ring_apply          3 payloads read; l, r read + written;
                       w read; t written; w written (t)        -> 3N + 7 x 2N = 17N
 
-  python bagua-core_amd/tools/ring_kernels_probe.py [--elements N] [--steps K] [--json out]
+  python tools/ring_kernels_probe.py [--elements N] [--steps K] [--json out]
 """
 import argparse
 import ctypes
@@ -25,7 +25,7 @@ import sys
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "bagua-core_amd"))
 
 from bagua_core import _native as N  # noqa: E402
 

@@ -3,7 +3,7 @@
 communicator, ms per step (run under rocprofv3 --kernel-trace --stats for the
 per-kernel split).
 
-  python bagua-core_amd/tools/ring_probe.py [--elements N] [--steps K] [--pieces P]
+  python tools/ring_probe.py [--elements N] [--steps K] [--pieces P]
 """
 import argparse
 import ctypes
@@ -14,7 +14,7 @@ import time
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "bagua-core_amd"))
 
 import bagua_core  # noqa: E402
 from bagua_core import _native as N  # noqa: E402

@@ -4,7 +4,7 @@ iterations, then the pipelined op and the 1-bit op at one rank; prints the devic
 in-use / cached / pending bytes and the stream-workspace count every N iterations, so growth
 (leaked pool blocks, events, workspaces) shows.
 
-    python bagua-core_amd/tools/soak_probe.py [--iters 400]
+    python tools/soak_probe.py [--iters 400]
 """
 import argparse
 import ctypes
@@ -15,7 +15,7 @@ import time
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "bagua-core_amd"))
 
 
