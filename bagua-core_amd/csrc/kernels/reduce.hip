@@ -286,8 +286,9 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
     static_assert(STORE || PARTIALS, "a pass that neither stores nor reduces does nothing");
-    __shared__ QParams qp[kMaxFusedChunks];
-    __shared__ float lut[kMaxFusedChunks][256];
+    // reduce_by(p) = BY keeps p <= 2 BY: tables for 2 BY segments (4 KiB at p <= 4)
+    __shared__ QParams qp[2 * BY];
+    __shared__ float lut[2 * BY][256];
     build_luts<T>(in, chunk_offset, p, qp, lut);
     uint32_t lo = min_space(T::init_max()), hi = max_space(-T::init_max());
     reduce_tiles<T, BY, AV, PF>(
@@ -340,8 +341,8 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
     int64_t e0, int64_t cs_total) {
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
-    __shared__ QParams qp[kMaxFusedChunks];
-    __shared__ float lut[kMaxFusedChunks][256];
+    __shared__ QParams qp[2 * BY];  // p <= 2 BY, as in dequant_reduce_kernel
+    __shared__ float lut[2 * BY][256];
     uint32_t lo = 0xffffffffu, hi = 0xffffffffu;
     for (int i = threadIdx.x; i < npartials; i += kBlock) {
         const uint2 pr = partials[i];

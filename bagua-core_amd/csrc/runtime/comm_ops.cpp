@@ -562,12 +562,17 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
         HIP2(hipEventRecord(exchanged[q], s1));
     }
     // 2. reduce the p received versions of the own chunk piece by piece, requantise it.
-    // By default the reduced chunk is not stored: each reduce piece emits its min/max
-    // partials only and the requantise recomputes the piece from the received segments
-    // ((2p + 1) L bytes per piece instead of (p + 9) L at fp32; the own chunk of x is
-    // rewritten by the final dequantise anyway).  BAGUA_PIPE_RECOMPUTE=0: the storing
-    // pair (A/B).
-    const bool recompute = env_int("BAGUA_PIPE_RECOMPUTE", 1) != 0;
+    // The reduced chunk need not be stored (the final dequantise rewrites the own chunk
+    // of x): with `recompute` each reduce piece emits its min/max partials only and the
+    // requantise recomputes the piece from the received segments, (2p + 1) L bytes per
+    // piece of L elements instead of (p + 2 sizeof(T) + 1) L, at twice the table
+    // lookups.  Measured on 1 GiB fp32 (tools/pipeline_kernels_probe.py,
+    // profiles/r06_pipe_probe_p{4,8}.json) it pays at p = 2 only -- the middle step 71.0
+    // -> 58.0 us with 4 pieces, 42.6 -> 35.4 with 8 -- and loses from p = 4 on (the
+    // lookups, not the bytes, bound these kernels), so it runs where 2p <= sizeof(T).
+    // BAGUA_PIPE_RECOMPUTE=0 / 1 forces either (A/B).
+    const int rc_env = env_int("BAGUA_PIPE_RECOMPUTE", -1);
+    const bool recompute = rc_env >= 0 ? rc_env != 0 : 2 * (size_t)p <= bagua_dtype_bytes(dt);
     for (int q = 0; q < pieces; ++q) {
         HIP2(hipStreamWaitEvent(s0, exchanged[q], 0));
         TRY2(bagua_minmax_u8_reduce_piece(dt, rb, k.S, cs, p, recompute ? nullptr : x, average, k.rank, sched, q, ws,

@@ -106,6 +106,39 @@ def main():
         row["prefix_us"] = round(row["minmax_pass_us"] + q_us[0], 1)
         row["store"]["middle_us"] = round(r_us[-1] + rq_us[0], 1)
         row["recompute"]["middle_us"] = round(r2_us[-1] + rq2_us[0], 1)
+        # the op's order since round 6: the LAST piece is requantised (and gathered) first,
+        # right after its reduce, while its bytes are still in the caches
+        # In the op the requantise follows the reduce pieces, not itself: time it (and the
+        # last reduce piece) in that order from a flushed Infinity Cache, requantising piece
+        # 0 first (round 5's order) or the last piece first (round 6's)
+        flush = torch.empty(1 << 29, dtype=torch.uint8, device=dev)
+
+        def in_order(store, first):
+            ts = []
+            for _ in range(a.reps):
+                flush.add_(1)  # 512 MiB read + written: the caches hold nothing of this op
+                for q in range(P - 1):
+                    K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp if store else None, 1, r, P, q, wp, wsb, sp)
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                e[0].record(st)
+                e[1].record(st)
+                N.check(K.bagua_time_next_kernel(e[0].cuda_event, e[1].cuda_event), "timing hook")
+                K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp if store else None, 1, r, P, P - 1, wp, wsb, sp)
+                e[2].record(st)
+                e[3].record(st)
+                N.check(K.bagua_time_next_kernel(e[2].cuda_event, e[3].cuda_event), "timing hook")
+                if store:
+                    K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, P, first, wp, wsb, sp)
+                else:
+                    K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, P, first, wp, wsb, sp)
+                torch.cuda.synchronize()
+                ts.append((e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3])) * 1e3)
+            ts.sort()
+            return round(ts[len(ts) // 2], 1)
+        for m, store in (("store", True), ("recompute", False)):
+            row[m]["middle_in_order_first_piece_us"] = in_order(store, 0)
+            row[m]["middle_in_order_last_piece_us"] = in_order(store, P - 1)
+        del flush
         row["suffix_us"] = round(d_us[-1], 1)
         common = row["minmax_pass_us"] + sum(q_us) + sum(d_us)
         row["store"]["codec_total_us"] = round(common + sum(r_us) + sum(rq_us), 1)
@@ -116,13 +149,13 @@ def main():
             K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp, 1, r, P, q, wp, wsb, sp)
         for q in range(P):
             K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, P, q, wp, wsb, sp)
-        a = send.clone()
+        snap = send.clone()
         for q in range(P):
             K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, None, 1, r, P, q, wp, wsb, sp)
         for q in range(P):
             K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, P, q, wp, wsb, sp)
         torch.cuda.synchronize()
-        row["recompute_bytes_equal"] = bool(torch.equal(a, send))
+        row["recompute_bytes_equal"] = bool(torch.equal(snap, send))
         del recv
         row["minmax_pass_us"] = round(row["minmax_pass_us"], 1)
         out[f"p{p}"] = row
