@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pieces", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--tapered", action="store_true", help="first and last piece half size (PIECES_TAPERED)")
     a = ap.parse_args()
     from bagua_core import _native as N
     K = N.K
@@ -34,7 +35,7 @@ def main():
     x = torch.randn(n, device=dev, generator=g) * 1e-3
     st = torch.cuda.current_stream()
     sp = ctypes.c_void_p(st.cuda_stream)
-    out = {"bucket_bytes": 4 * n, "pieces": a.pieces}
+    out = {"bucket_bytes": 4 * n, "pieces": a.pieces, "tapered": a.tapered}
 
     def timed(call):
         ts = []
@@ -52,8 +53,9 @@ def main():
     for p in (2, 4, 8):
         cs = n // p
         P = a.pieces
+        SCH = P | (N.PIECES_TAPERED if a.tapered else 0)  # the piece schedule every piece call takes
         S = K.bagua_minmax_u8_compressed_bytes(0, cs, p)
-        wsb = max(K.bagua_minmax_u8_workspace_bytes(cs, p), K.bagua_minmax_u8_pipeline_workspace_bytes(cs, P))
+        wsb = max(K.bagua_minmax_u8_workspace_bytes(cs, p), K.bagua_minmax_u8_pipeline_workspace_bytes(cs, SCH))
         send = torch.empty(S, dtype=torch.uint8, device=dev)
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
         xp, cp, wp = x.data_ptr(), send.data_ptr(), ws.data_ptr()
@@ -61,7 +63,7 @@ def main():
 
         def rng(q):
             b, e = ctypes.c_int(), ctypes.c_int()
-            N.check(K.bagua_minmax_u8_piece_range(cs, P, q, ctypes.byref(b), ctypes.byref(e)), "range")
+            N.check(K.bagua_minmax_u8_piece_range(cs, SCH, q, ctypes.byref(b), ctypes.byref(e)), "range")
             return b.value, e.value
         row = {}
         row["minmax_pass_us"] = timed(lambda: K.bagua_minmax_u8_compress_stage(5, 0, xp, n, cs, p, cp, S, wp, wsb, -1,
@@ -74,14 +76,14 @@ def main():
         rp = recv.data_ptr()
         # storing pair (BAGUA_PIPE_RECOMPUTE=0): the reduce piece stores the reduced piece of
         # the own chunk (4 B per element) and the requantise reads it back
-        r_us = [timed(lambda q=q: K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp, 1, r, P, q, wp, wsb, sp))
+        r_us = [timed(lambda q=q: K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp, 1, r, SCH, q, wp, wsb, sp))
                 for q in range(P)]
-        rq_us = [timed(lambda q=q: K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, P, q, wp, wsb, sp))
+        rq_us = [timed(lambda q=q: K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, SCH, q, wp, wsb, sp))
                  for q in range(P)]
         # the op's default: partials-only reduce pieces, the requantise recomputes from recv
-        r2_us = [timed(lambda q=q: K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, None, 1, r, P, q, wp, wsb, sp))
+        r2_us = [timed(lambda q=q: K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, None, 1, r, SCH, q, wp, wsb, sp))
                  for q in range(P)]
-        rq2_us = [timed(lambda q=q: K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, P, q, wp,
+        rq2_us = [timed(lambda q=q: K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, SCH, q, wp,
                                                                               wsb, sp))
                   for q in range(P)]
         d_us = [timed(lambda q=q: K.bagua_minmax_u8_decompress_range(0, cp, S, cs, p, xp, *rng(q), sp))
@@ -118,19 +120,19 @@ def main():
             for _ in range(a.reps):
                 flush.add_(1)  # 512 MiB read + written: the caches hold nothing of this op
                 for q in range(P - 1):
-                    K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp if store else None, 1, r, P, q, wp, wsb, sp)
+                    K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp if store else None, 1, r, SCH, q, wp, wsb, sp)
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
                 e[0].record(st)
                 e[1].record(st)
                 N.check(K.bagua_time_next_kernel(e[0].cuda_event, e[1].cuda_event), "timing hook")
-                K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp if store else None, 1, r, P, P - 1, wp, wsb, sp)
+                K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp if store else None, 1, r, SCH, P - 1, wp, wsb, sp)
                 e[2].record(st)
                 e[3].record(st)
                 N.check(K.bagua_time_next_kernel(e[2].cuda_event, e[3].cuda_event), "timing hook")
                 if store:
-                    K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, P, first, wp, wsb, sp)
+                    K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, SCH, first, wp, wsb, sp)
                 else:
-                    K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, P, first, wp, wsb, sp)
+                    K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, SCH, first, wp, wsb, sp)
                 torch.cuda.synchronize()
                 ts.append((e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3])) * 1e3)
             ts.sort()
@@ -144,16 +146,16 @@ def main():
         row["store"]["codec_total_us"] = round(common + sum(r_us) + sum(rq_us), 1)
         row["recompute"]["codec_total_us"] = round(common + sum(r2_us) + sum(rq2_us), 1)
         # the recompute requantise writes the same bytes as the storing pair
-        K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp, 1, r, P, 0, wp, wsb, sp)
+        K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp, 1, r, SCH, 0, wp, wsb, sp)
         for q in range(P):
-            K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp, 1, r, P, q, wp, wsb, sp)
+            K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp, 1, r, SCH, q, wp, wsb, sp)
         for q in range(P):
-            K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, P, q, wp, wsb, sp)
+            K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, SCH, q, wp, wsb, sp)
         snap = send.clone()
         for q in range(P):
-            K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, None, 1, r, P, q, wp, wsb, sp)
+            K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, None, 1, r, SCH, q, wp, wsb, sp)
         for q in range(P):
-            K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, P, q, wp, wsb, sp)
+            K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, SCH, q, wp, wsb, sp)
         torch.cuda.synchronize()
         row["recompute_bytes_equal"] = bool(torch.equal(snap, send))
         del recv
