@@ -148,8 +148,8 @@ GiB = float(1 << 30)
 SIDE_TIMEOUT_S = 120.0  # N > 1 side measurements: abort the communicator instead of hanging
 MIN_SIDE_S = 10.0  # N > 1: a side line starts only with this much of --budget-s left
 HEADLINE_TIMEOUT_S = 300.0  # N > 1 headline (pipelined op): abort, then measure the unpieced op
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")
-PMC_SUMMARY_ONEBIT = os.path.join(ROOT, "profiles", "r05_pmc_traffic_onebit.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06_pmc_traffic.json")
+PMC_SUMMARY_ONEBIT = os.path.join(ROOT, "profiles", "r06_pmc_traffic_onebit.json")
 
 
 def parse():
