@@ -513,15 +513,16 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     const bool vec = ((uintptr_t)chunk % (4 * sizeof(S))) == 0;
     uint8_t* bits = out_seg + 32;
-    for (int64_t t = wave; t < tiles; t += nwaves) {
-        // every segment's 16-bit field of this lane, loaded unconditionally (segments
-        // >= p read the last one and are masked to 0 after the loads)
-        uint32_t f[PMAX];
+    // every segment's 16-bit field of this lane for tile t, loaded unconditionally
+    // (segments >= p read the last one and are masked to 0 after the loads)
+    auto load_fields = [&](int64_t t, uint32_t (&f)[PMAX]) {
 #pragma unroll
         for (int c = 0; c < PMAX; ++c) {
             const int cc = c < p ? c : p - 1;
             f[c] = reinterpret_cast<const uint16_t*>(in + (int64_t)cc * chunk_offset + 32 + t * kObTileBytes)[lane];
         }
+    };
+    auto process = [&](int64_t t, uint32_t (&f)[PMAX]) {
 #pragma unroll
         for (int c = 0; c < PMAX; ++c) f[c] = c < p ? f[c] : 0u;
         float x[4][4];
@@ -537,8 +538,9 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
                 x[b / 4][b % 4] = as_stored<T>(average ? v / pf : v);
             }
         } else if constexpr (PMAX == 2) {
+            const uint32_t g = f[0] | (f[1] << 16);  // bit b: segment 0 at b, segment 1 at b + 16
 #pragma unroll
-            for (int b = 0; b < 16; ++b) x[b / 4][b % 4] = lut[0][((f[0] >> b) & 1u) | (((f[1] >> b) & 1u) << 1)];
+            for (int b = 0; b < 16; ++b) x[b / 4][b % 4] = lut[0][((g >> b) & 1u) | ((g >> (b + 15)) & 2u)];
         } else {
             uint32_t rows[8], ix[16];
 #pragma unroll
@@ -547,15 +549,18 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
 #pragma unroll
             for (int b = 0; b < 16; ++b) x[b / 4][b % 4] = lut[0][ix[b]];
         }
+        if ((t + 1) * kObTile > cs) {  // the ragged last tile: padding past cs stays 0 (as the encoder sees it)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (t * kObTile + k * 256 + lane * 4 + e >= cs) x[k][e] = 0.0f;
+        }
         uint32_t field = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t j = t * kObTile + k * 256 + lane * 4 + e;
-                if (j >= cs) x[k][e] = 0.0f;  // padding past cs stays 0 (as the encoder sees it)
-                field |= (x[k][e] < 0.0f ? 1u : 0u) << (k * 4 + e);
-            }
+            for (int e = 0; e < 4; ++e) field |= (x[k][e] < 0.0f ? 1u : 0u) << (k * 4 + e);
         if constexpr (STORE) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) store4<T>(chunk, t * kObTile + k * 256 + lane * 4, cs, vec, x[k]);
@@ -569,6 +574,21 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
             for (int e = 0; e < 4; ++e) ab[k][e] = __builtin_fabsf(x[k][e]);
         const float sum = wave_tree_sum(lane_tree(ab));
         if (lane == 0) part[t] = sum;
+    };
+    // U tiles per wave iteration, all their loads issued before the first is used: at
+    // p <= 2 a tile's input is 4 B per lane, and one tile at a time kept a wave waiting a
+    // whole memory latency per 1,024 elements (1 GiB, p = 2: 46.5 -> 39.0 us with U = 4).
+    // The transposing paths keep one tile (U = 4 there: p = 4 30.7 -> 33.0, p = 8
+    // 18.9 -> 22.7 us; profiles/r06_onebit_middle_unroll.json)
+    constexpr int U = PMAX == 2 ? 4 : 1;
+    for (int64_t t0 = wave; t0 < tiles; t0 += U * nwaves) {
+        uint32_t f[U][PMAX];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (t0 + u * nwaves < tiles) load_fields(t0 + u * nwaves, f[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (t0 + u * nwaves < tiles) process(t0 + u * nwaves, f[u]);
     }
 }
 
