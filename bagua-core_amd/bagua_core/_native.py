@@ -35,7 +35,7 @@ except ImportError as _e:
 DTYPE_F32, DTYPE_F16, DTYPE_BF16, DTYPE_U8, DTYPE_I64, DTYPE_U64 = 0, 1, 2, 3, 4, 5
 COMPRESSION_NONE, COMPRESSION_MINMAX_UINT8, COMPRESSION_ONEBIT = 0, 1, 2
 # piece schedules (bagua_kernels.h): a count, optionally OR-ed with PIECES_TAPERED
-PIECES_COUNT_MASK, PIECES_TAPERED, PIECES_MULTIPATH = 0xFFFF, 0x10000, 0x20000
+PIECES_COUNT_MASK, PIECES_TAPERED, PIECES_MULTIPATH, PIECES_FOLDED = 0xFFFF, 0x10000, 0x20000, 0x40000
 OP_SUM, OP_PROD, OP_MIN, OP_MAX, OP_AVG = 0, 1, 2, 3, 10
 
 STATUS = {0: "ok", 1: "invalid argument", 2: "workspace too small", 3: "HIP launch failed",
@@ -108,6 +108,7 @@ KERNEL_SIGNATURES = {
     "bagua_minmax_u8_requantize_piece": (_i32, [_i32, _vp, _i32, _i32, _vp, _sz, _i32, _i32, _i32, _vp, _sz, _vp]),
     "bagua_minmax_u8_reduce_requantize_piece": (_i32, [_i32, _vp, _sz, _i32, _i32, _i32, _vp, _sz, _i32, _i32, _i32,
                                                         _vp, _sz, _vp]),
+    "bagua_minmax_u8_fold_piece_partials": (_i32, [_i32, _i32, _i32, _vp, _sz, _vp]),
     "bagua_ring_mix_minmax": (_i32, [_i32, _vp, _vp, _vp, _vp, _i32, _vp, _sz, _vp]),
     "bagua_ring_apply_minmax": (_i32, [_i32, _vp, _vp, _vp, _sz, _i32, _vp, _vp, _vp, _vp, _vp]),
     "bagua_ring_apply_minmax_range": (_i32, [_i32, _vp, _vp, _vp, _sz, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),

@@ -678,7 +678,8 @@ static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs
 // so every rank and every building block of one op sees the same ranges.
 static bool piece_schedule_ok(int pieces) {
     const int n = pieces & BAGUA_PIECES_COUNT_MASK;
-    return n >= 1 && (pieces & ~(BAGUA_PIECES_COUNT_MASK | BAGUA_PIECES_TAPERED | BAGUA_PIECES_MULTIPATH)) == 0;
+    return n >= 1 && (pieces & ~(BAGUA_PIECES_COUNT_MASK | BAGUA_PIECES_TAPERED | BAGUA_PIECES_MULTIPATH |
+                                 BAGUA_PIECES_FOLDED)) == 0;
 }
 static int piece_count(int pieces) { return pieces & BAGUA_PIECES_COUNT_MASK; }
 
@@ -714,6 +715,46 @@ static int piece_blocks(int cs, int schedule, int per_vec) {
 // tensor == nullptr: the piece's min/max partials only, nothing stored (the
 // requantise then recomputes the piece from the received segments:
 // reduce_requantize_piece_impl)
+// the one folded partial (bagua_minmax_u8_fold_piece_partials) sits after the largest
+// partials region any dtype writes (f32's, 4 elements per vector) -- inside the
+// workspace's 256-byte tail
+static uint2* folded_slot(void* ws, int cs, int pieces) {
+    return static_cast<uint2*>(ws) + (size_t)piece_count(pieces) * piece_blocks(cs, pieces, 4);
+}
+
+// one workgroup folds n {min, max} key partials into out[0]
+__global__ __launch_bounds__(kBlock) void fold_partials_kernel(const uint2* __restrict__ in, int64_t n,
+                                                               uint2* __restrict__ out) {
+    uint32_t lo = 0xffffffffu, hi = 0xffffffffu;
+    for (int64_t i = threadIdx.x; i < n; i += kBlock) {
+        const uint2 v = in[i];
+        lo = min(lo, v.x);
+        hi = min(hi, v.y);
+    }
+    lo = wave_umin(lo);
+    hi = wave_umin(hi);
+    __shared__ uint32_t red[2][kWavesPerBlock];
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 0) { red[0][w] = lo; red[1][w] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 1; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
+        out[0] = make_uint2(lo, hi);
+    }
+}
+
+template <typename T>
+static int fold_piece_partials_impl(int cs, int pieces, void* ws, size_t ws_bytes, hipStream_t s) {
+    if (cs < 0 || !piece_schedule_ok(pieces)) return BAGUA_ERR_INVALID_ARG;
+    const int blocks = piece_blocks(cs, pieces, Vec<T>::N);
+    const int n = piece_count(pieces) * blocks;
+    uint2* slot = ws ? folded_slot(ws, cs, pieces) : nullptr;
+    if (!ws || (uint8_t*)(slot + 1) > (uint8_t*)ws + ws_bytes) return BAGUA_ERR_WORKSPACE;
+    launch(fold_partials_kernel, dim3(1), dim3(kBlock), 0, s, static_cast<const uint2*>(ws), (int64_t)n, slot);
+    return check_launch();
+}
+
 template <typename T>
 static int reduce_piece_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, void* tensor, int average,
                              int target, int pieces, int piece, void* ws, size_t ws_bytes, hipStream_t s) {
@@ -748,14 +789,16 @@ static int reduce_requantize_piece_impl(const uint8_t* recv, size_t recv_bytes, 
     const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     const int blocks = piece_blocks(cs, pieces, Vec<T>::N);
-    const int partials = piece_count(pieces) * blocks;
-    if (!ws || ws_bytes < (size_t)partials * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
+    const bool folded = (pieces & BAGUA_PIECES_FOLDED) != 0;
+    const int partials = folded ? 1 : piece_count(pieces) * blocks;
+    const uint2* part = folded ? folded_slot(const_cast<void*>(ws), cs, pieces) : static_cast<const uint2*>(ws);
+    if (!ws || ws_bytes < (size_t)((const uint8_t*)(part + partials) - (const uint8_t*)ws)) return BAGUA_ERR_WORKSPACE;
     int b, e;
     piece_range(cs, pieces, piece, &b, &e);
     if (b == e && piece > 0) return BAGUA_OK;  // empty trailing piece: its bytes were written by the others
     const int grid = (int)std::min<int64_t>(fused_blocks(e - b, Vec<T>::N),
                                             tune_int("BAGUA_TUNE_RRQ_BLOCKS", fold_grid_target(partials)));
-    return dequant_reduce_quantize_impl<T>(recv, recv_bytes, cs, p, average, static_cast<const uint2*>(ws), partials,
+    return dequant_reduce_quantize_impl<T>(recv, recv_bytes, cs, p, average, part, partials,
                                            out + (int64_t)target * chunk_offset, chunk_offset, grid, s, nullptr, b,
                                            e);
 }
@@ -775,12 +818,14 @@ static int requantize_pieces_impl(const void* tensor, int cs, int p, uint8_t* ou
     const int64_t chunk_offset = (int64_t)(out_bytes / (size_t)p);
     if (chunk_offset < (int64_t)cs + 32) return BAGUA_ERR_INVALID_ARG;
     const int blocks = piece_blocks(cs, pieces, Vec<T>::N);
-    const int partials = piece_count(pieces) * blocks;
-    if (!ws || ws_bytes < (size_t)partials * sizeof(uint2)) return BAGUA_ERR_WORKSPACE;
+    const bool folded = (pieces & BAGUA_PIECES_FOLDED) != 0;
+    const int partials = folded ? 1 : piece_count(pieces) * blocks;
+    const uint2* part = folded ? folded_slot(const_cast<void*>(ws), cs, pieces) : static_cast<const uint2*>(ws);
+    if (!ws || ws_bytes < (size_t)((const uint8_t*)(part + partials) - (const uint8_t*)ws)) return BAGUA_ERR_WORKSPACE;
     launch((minmax_quantize_kernel<T, true>),
            dim3(blocks_for(e1 - e0, Vec<T>::N, 1, kSubtiles, fold_grid_target(partials)), 1), dim3(kBlock), 0,
            s, static_cast<const S*>(tensor), (int64_t)p * cs, (int64_t)cs, (int64_t)e0, (int64_t)e1, target,
-           static_cast<const uint2*>(ws), partials, out, chunk_offset, (int64_t)out_bytes, p);
+           part, partials, out, chunk_offset, (int64_t)out_bytes, p);
     return check_launch();
 }
 
@@ -1013,6 +1058,12 @@ int bagua_minmax_u8_reduce_requantize_piece(int dtype, const uint8_t* input, siz
     BAGUA_DTYPE_DISPATCH(dtype, reduce_requantize_piece_impl<T>(input, input_bytes, chunk_size, num_chunks, average,
                                                                 output, output_bytes, target_chunk, pieces, piece,
                                                                 workspace, workspace_bytes, s));
+}
+
+int bagua_minmax_u8_fold_piece_partials(int dtype, int chunk_size, int pieces, void* workspace, size_t workspace_bytes,
+                                        bagua_stream_t stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    BAGUA_DTYPE_DISPATCH(dtype, fold_piece_partials_impl<T>(chunk_size, pieces, workspace, workspace_bytes, s));
 }
 
 int bagua_minmax_u8_requantize_pieces(int dtype, const void* tensor, int chunk_size, int num_chunks, uint8_t* output,

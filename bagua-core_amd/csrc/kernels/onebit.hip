@@ -481,7 +481,7 @@ __device__ __forceinline__ float lut_half(int bits, int parity, int p, const flo
 }
 
 // PMAX = 2: p <= 2, the index is read bit by bit; 8: the 8x8 transpose; 16: two tables
-template <typename T, int PMAX, bool STORE>
+template <typename T, int PMAX, bool STORE, int UT = (PMAX == 2 ? 4 : 1)>
 __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
     const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int p, int average,
     typename T::storage* __restrict__ chunk, uint8_t* __restrict__ out_seg, float* __restrict__ part) {
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
     // whole memory latency per 1,024 elements (1 GiB, p = 2: 46.5 -> 39.0 us with U = 4).
     // The transposing paths keep one tile (U = 4 there: p = 4 30.7 -> 33.0, p = 8
     // 18.9 -> 22.7 us; profiles/r06_onebit_middle_unroll.json)
-    constexpr int U = PMAX == 2 ? 4 : 1;
+    constexpr int U = UT;
     for (int64_t t0 = wave; t0 < tiles; t0 += U * nwaves) {
         uint32_t f[U][PMAX];
 #pragma unroll
@@ -816,6 +816,19 @@ static void launch_ob_reduce(const uint8_t* in, int64_t co, int64_t cs, int p, t
 template <typename T, int PMAX>
 static void launch_ob_reduce_lut(const uint8_t* in, int64_t co, int64_t cs, int p, int average,
                                  typename T::storage* chunk, uint8_t* seg, float* part, int blocks, hipStream_t s) {
+    if constexpr (PMAX == 2) {  // tiles per wave iteration at p <= 2: BAGUA_OB_MIDDLE_U (A/B; default 4)
+        const int u = tune_int("BAGUA_OB_MIDDLE_U", 4);
+        if (!chunk && u == 2) {
+            launch(onebit_reduce_encode_lut_kernel<T, 2, false, 2>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
+                   average, chunk, seg, part);
+            return;
+        }
+        if (!chunk && u == 8) {
+            launch(onebit_reduce_encode_lut_kernel<T, 2, false, 8>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
+                   average, chunk, seg, part);
+            return;
+        }
+    }
     if (chunk)
         launch(onebit_reduce_encode_lut_kernel<T, PMAX, true>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
                average, chunk, seg, part);
@@ -844,7 +857,7 @@ static int ob_reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int
         return !(v && v[0] == '0');
     }();
     if (tiles > 0 && lut_on) {
-        const int blocks = ob_blocks(tiles, 1);
+        const int blocks = ob_blocks(tiles, 1, tune_int("BAGUA_TUNE_OB_MIDDLE_BLOCKS", kTargetBlocks));
         if (p <= 2)
             launch_ob_reduce_lut<T, 2>(recv, co_in, cs, p, average, chunk, seg, part, blocks, s);
         else if (p <= 8)

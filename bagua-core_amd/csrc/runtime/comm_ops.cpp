@@ -578,14 +578,20 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
         TRY2(bagua_minmax_u8_reduce_piece(dt, rb, k.S, cs, p, recompute ? nullptr : x, average, k.rank, sched, q, ws,
                                           ws_bytes, s0));
     }
-    // requantise piece by piece (each folds every piece's partials), so the allgather of
-    // piece q starts while piece q+1 is requantised
+    // requantise piece by piece, so the allgather of piece q starts while piece q+1 is
+    // requantised.  Every requantise needs the whole chunk's min/max: one workgroup first
+    // folds all pieces' partials into one value (BAGUA_PIECES_FOLDED), so the requantise
+    // workgroups read one value each instead of pieces x 2,048 partials
+    // (BAGUA_PIPE_PREFOLD=0: every workgroup folds them itself, A/B)
+    const bool prefold = env_int("BAGUA_PIPE_PREFOLD", 1) != 0;
+    if (prefold) TRY2(bagua_minmax_u8_fold_piece_partials(dt, cs, sched, ws, ws_bytes, s0));
+    const int rq_sched = sched | (prefold ? BAGUA_PIECES_FOLDED : 0);
     for (int q = 0; q < pieces; ++q) {
         if (recompute)
-            TRY2(bagua_minmax_u8_reduce_requantize_piece(dt, rb, k.S, cs, p, average, sb, k.S, k.rank, sched, q, ws,
+            TRY2(bagua_minmax_u8_reduce_requantize_piece(dt, rb, k.S, cs, p, average, sb, k.S, k.rank, rq_sched, q, ws,
                                                          ws_bytes, s0));
         else
-            TRY2(bagua_minmax_u8_requantize_piece(dt, x, cs, p, sb, k.S, k.rank, sched, q, ws, ws_bytes, s0));
+            TRY2(bagua_minmax_u8_requantize_piece(dt, x, cs, p, sb, k.S, k.rank, rq_sched, q, ws, ws_bytes, s0));
         HIP2(hipEventRecord(requantised_piece[q], s0));
     }
     // 3. allgather + dequantise piece by piece

@@ -243,6 +243,9 @@ int bagua_onebit_centralized_one_rank(int dtype, void* tensor, int num_elem, int
 /* decentralized ring op only: the relayed (multipath) exchange from 6 ranks on
  * (the reference's direct exchange otherwise); ignored by the piece functions */
 #define BAGUA_PIECES_MULTIPATH 0x20000
+/* requantise calls only: every piece's min/max partials were already folded into one
+ * (bagua_minmax_u8_fold_piece_partials), so each requantise workgroup reads one value */
+#define BAGUA_PIECES_FOLDED 0x40000
 int bagua_minmax_u8_piece_range(int chunk_size, int pieces, int piece, int* begin, int* end);
 size_t bagua_minmax_u8_pipeline_workspace_bytes(int chunk_size, int pieces);
 int bagua_minmax_u8_quantize_range(int dtype, const void* input, int input_num_element, int chunk_size,
@@ -274,6 +277,12 @@ int bagua_minmax_u8_reduce_requantize_piece(int dtype, const uint8_t* input, siz
                                             int num_chunks, int average, uint8_t* output, size_t output_bytes,
                                             int target_chunk, int pieces, int piece, const void* workspace,
                                             size_t workspace_bytes, bagua_stream_t stream);
+/* Fold every piece's min/max partials (written by bagua_minmax_u8_reduce_piece) into one
+ * value in the workspace, after the last reduce piece; the requantise calls that follow
+ * pass `pieces | BAGUA_PIECES_FOLDED` and read that one value instead of folding
+ * pieces x workgroups partials in every workgroup. */
+int bagua_minmax_u8_fold_piece_partials(int dtype, int chunk_size, int pieces, void* workspace, size_t workspace_bytes,
+                                        bagua_stream_t stream);
 
 /* Decentralized ring op (decentralized_low_precision_synchronous.rs:45-64,126-151)
  * as two fused passes around the MinMax quantise pass, bit-identical to the

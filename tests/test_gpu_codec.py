@@ -16,6 +16,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 F32, F16, BF16 = 0, 1, 2
+PIECES_FOLDED = 0x40000  # bagua_kernels.h BAGUA_PIECES_FOLDED
 STORAGE = {F32: np.float32, F16: np.float16, BF16: np.uint16}
 TORCH = {F32: torch.float32, F16: torch.float16, BF16: torch.bfloat16}
 
@@ -261,9 +262,10 @@ def test_fused_reduce_requantize(bc, oracle_c, dtype, p, ragged, mode, average):
     assert np.all(got[other] == 0xA5), "bytes outside the target segment written"
 
 
-def recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces, ws, send_want, t_untouched=False):
+def recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces, ws, send_want, t_untouched=False, prefold=False):
     """bagua_minmax_u8_reduce_piece(tensor = NULL) per piece, then
-    bagua_minmax_u8_reduce_requantize_piece per piece (reverse order): segment r equals the
+    bagua_minmax_u8_reduce_requantize_piece per piece (reverse order; with `prefold` after
+    bagua_minmax_u8_fold_piece_partials, as PIECES_FOLDED): segment r equals the
     oracle's decompress + reduce_mean + compress(target), no other byte is written."""
     co = S // p
     send_d = torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
@@ -271,9 +273,13 @@ def recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces, ws, send_want, t_unt
     for q in range(n):
         assert K.bagua_minmax_u8_reduce_piece(dtype, recv_d.data_ptr(), S, cs, p, None, 1, r, pieces, q,
                                               ws.data_ptr(), ws.numel(), None) == 0
+    rq = pieces
+    if prefold:
+        assert K.bagua_minmax_u8_fold_piece_partials(dtype, cs, pieces, ws.data_ptr(), ws.numel(), None) == 0
+        rq = pieces | PIECES_FOLDED
     for q in reversed(range(n)):
         assert K.bagua_minmax_u8_reduce_requantize_piece(dtype, recv_d.data_ptr(), S, cs, p, 1, send_d.data_ptr(), S,
-                                                         r, pieces, q, ws.data_ptr(), ws.numel(), None) == 0
+                                                         r, rq, q, ws.data_ptr(), ws.numel(), None) == 0
     got = send_d.cpu().numpy()
     assert np.array_equal(got[r * co:(r + 1) * co], send_want[r * co:(r + 1) * co]), (p, pieces)
     assert np.all(np.delete(got, np.s_[r * co:(r + 1) * co]) == 0xA5)
@@ -331,8 +337,21 @@ def test_minmax_piecewise_building_blocks(bc, oracle_c, dtype, p, pieces):
     # 2b. the op's default middle step: partials-only reduce pieces, then every piece
     # requantised straight from the received segments (tensor untouched), same bytes
     recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces, ws, send_want, t_untouched=True)
+    recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces, ws, send_want, prefold=True)
     if pieces >= 3:  # the tapered schedule (first and last piece half size)
         recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces | bc._native.PIECES_TAPERED, ws, send_want)
+    # the storing pair with the partials folded once (PIECES_FOLDED)
+    t2 = torch.zeros(p * cs, dtype=TORCH[dtype], device="cuda")
+    send2 = torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
+    for q in range(pieces):
+        assert K.bagua_minmax_u8_reduce_piece(dtype, recv_d.data_ptr(), S, cs, p, t2.data_ptr(), 1, r, pieces, q,
+                                              ws.data_ptr(), ws.numel(), None) == 0
+    assert K.bagua_minmax_u8_fold_piece_partials(dtype, cs, pieces, ws.data_ptr(), ws.numel(), None) == 0
+    for q in range(pieces):
+        assert K.bagua_minmax_u8_requantize_piece(dtype, t2.data_ptr(), cs, p, send2.data_ptr(), S, r,
+                                                  pieces | PIECES_FOLDED, q, ws.data_ptr(), ws.numel(), None) == 0
+    got2 = send2.cpu().numpy()
+    assert np.array_equal(got2[r * co:(r + 1) * co], send_want[r * co:(r + 1) * co])
     # 3. decompress, piece by piece
     y_d = torch.zeros(p * cs, dtype=TORCH[dtype], device="cuda")
     for q in range(pieces):

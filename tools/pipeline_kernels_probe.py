@@ -115,31 +115,37 @@ def main():
         # 0 first (round 5's order) or the last piece first (round 6's)
         flush = torch.empty(1 << 29, dtype=torch.uint8, device=dev)
 
-        def in_order(store, first):
+        def in_order(store, first, prefold=False):
             ts = []
             for _ in range(a.reps):
                 flush.add_(1)  # 512 MiB read + written: the caches hold nothing of this op
                 for q in range(P - 1):
                     K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp if store else None, 1, r, SCH, q, wp, wsb, sp)
-                e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-                e[0].record(st)
-                e[1].record(st)
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+                for ev in e:
+                    ev.record(st)
                 N.check(K.bagua_time_next_kernel(e[0].cuda_event, e[1].cuda_event), "timing hook")
                 K.bagua_minmax_u8_reduce_piece(0, rp, S, cs, p, xp if store else None, 1, r, SCH, P - 1, wp, wsb, sp)
-                e[2].record(st)
-                e[3].record(st)
+                rs = SCH
+                if prefold:  # one workgroup folds every piece's partials; the requantise reads one value
+                    N.check(K.bagua_time_next_kernel(e[4].cuda_event, e[5].cuda_event), "timing hook")
+                    N.check(K.bagua_minmax_u8_fold_piece_partials(0, cs, SCH, wp, wsb, sp), "fold")
+                    rs = SCH | N.PIECES_FOLDED
                 N.check(K.bagua_time_next_kernel(e[2].cuda_event, e[3].cuda_event), "timing hook")
                 if store:
-                    K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, SCH, first, wp, wsb, sp)
+                    N.check(K.bagua_minmax_u8_requantize_piece(0, xp, cs, p, cp, S, r, rs, first, wp, wsb, sp), "rq")
                 else:
-                    K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, SCH, first, wp, wsb, sp)
+                    N.check(K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, rs, first, wp,
+                                                                      wsb, sp), "rrq")
                 torch.cuda.synchronize()
-                ts.append((e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3])) * 1e3)
+                t = e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3]) + (e[4].elapsed_time(e[5]) if prefold else 0)
+                ts.append(t * 1e3)
             ts.sort()
             return round(ts[len(ts) // 2], 1)
         for m, store in (("store", True), ("recompute", False)):
             row[m]["middle_in_order_first_piece_us"] = in_order(store, 0)
             row[m]["middle_in_order_last_piece_us"] = in_order(store, P - 1)
+            row[m]["middle_in_order_prefold_us"] = in_order(store, 0, prefold=True)
         del flush
         row["suffix_us"] = round(d_us[-1], 1)
         common = row["minmax_pass_us"] + sum(q_us) + sum(d_us)
@@ -158,6 +164,12 @@ def main():
             K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, SCH, q, wp, wsb, sp)
         torch.cuda.synchronize()
         row["recompute_bytes_equal"] = bool(torch.equal(snap, send))
+        N.check(K.bagua_minmax_u8_fold_piece_partials(0, cs, SCH, wp, wsb, sp), "fold")
+        for q in range(P):
+            K.bagua_minmax_u8_reduce_requantize_piece(0, rp, S, cs, p, 1, cp, S, r, SCH | N.PIECES_FOLDED, q, wp, wsb,
+                                                      sp)
+        torch.cuda.synchronize()
+        row["prefold_bytes_equal"] = bool(torch.equal(snap, send))
         del recv
         row["minmax_pass_us"] = round(row["minmax_pass_us"], 1)
         out[f"p{p}"] = row
