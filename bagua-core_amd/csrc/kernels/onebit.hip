@@ -481,7 +481,7 @@ __device__ __forceinline__ float lut_half(int bits, int parity, int p, const flo
 }
 
 // PMAX = 2: p <= 2, the index is read bit by bit; 8: the 8x8 transpose; 16: two tables
-template <typename T, int PMAX, bool STORE, int UT = (PMAX == 2 ? 4 : 1)>
+template <typename T, int PMAX, bool STORE, int UT = (PMAX == 2 ? 2 : 1)>
 __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
     const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int p, int average,
     typename T::storage* __restrict__ chunk, uint8_t* __restrict__ out_seg, float* __restrict__ part) {
@@ -577,7 +577,8 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
     };
     // U tiles per wave iteration, all their loads issued before the first is used: at
     // p <= 2 a tile's input is 4 B per lane, and one tile at a time kept a wave waiting a
-    // whole memory latency per 1,024 elements (1 GiB, p = 2: 46.5 -> 39.0 us with U = 4).
+    // whole memory latency per 1,024 elements (1 GiB, p = 2: 46.5 us; U = 2 / 4 / 8 with
+    // 4,096 workgroups 35.1 / 38.7 / 48.8 us, profiles/r06_sweeps/ob_middle_*.json).
     // The transposing paths keep one tile (U = 4 there: p = 4 30.7 -> 33.0, p = 8
     // 18.9 -> 22.7 us; profiles/r06_onebit_middle_unroll.json)
     constexpr int U = UT;
@@ -816,10 +817,15 @@ static void launch_ob_reduce(const uint8_t* in, int64_t co, int64_t cs, int p, t
 template <typename T, int PMAX>
 static void launch_ob_reduce_lut(const uint8_t* in, int64_t co, int64_t cs, int p, int average,
                                  typename T::storage* chunk, uint8_t* seg, float* part, int blocks, hipStream_t s) {
-    if constexpr (PMAX == 2) {  // tiles per wave iteration at p <= 2: BAGUA_OB_MIDDLE_U (A/B; default 4)
-        const int u = tune_int("BAGUA_OB_MIDDLE_U", 4);
-        if (!chunk && u == 2) {
-            launch(onebit_reduce_encode_lut_kernel<T, 2, false, 2>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
+    if constexpr (PMAX == 2) {  // tiles per wave iteration at p <= 2: BAGUA_OB_MIDDLE_U (A/B; default 2)
+        const int u = tune_int("BAGUA_OB_MIDDLE_U", 2);
+        if (!chunk && u == 1) {
+            launch(onebit_reduce_encode_lut_kernel<T, 2, false, 1>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
+                   average, chunk, seg, part);
+            return;
+        }
+        if (!chunk && u == 4) {
+            launch(onebit_reduce_encode_lut_kernel<T, 2, false, 4>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
                    average, chunk, seg, part);
             return;
         }
@@ -857,7 +863,9 @@ static int ob_reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int
         return !(v && v[0] == '0');
     }();
     if (tiles > 0 && lut_on) {
-        const int blocks = ob_blocks(tiles, 1, tune_int("BAGUA_TUNE_OB_MIDDLE_BLOCKS", kTargetBlocks));
+        // p <= 2: 4,096 workgroups (two tiles per wave iteration, above); the transposing
+        // paths are fastest at 2,048 (profiles/r06_sweeps/ob_middle_*.json)
+        const int blocks = ob_blocks(tiles, 1, tune_int("BAGUA_TUNE_OB_MIDDLE_BLOCKS", p <= 2 ? 4096 : kTargetBlocks));
         if (p <= 2)
             launch_ob_reduce_lut<T, 2>(recv, co_in, cs, p, average, chunk, seg, part, blocks, s);
         else if (p <= 8)

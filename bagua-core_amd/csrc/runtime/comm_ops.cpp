@@ -579,11 +579,12 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
                                           ws_bytes, s0));
     }
     // requantise piece by piece, so the allgather of piece q starts while piece q+1 is
-    // requantised.  Every requantise needs the whole chunk's min/max: one workgroup first
-    // folds all pieces' partials into one value (BAGUA_PIECES_FOLDED), so the requantise
-    // workgroups read one value each instead of pieces x 2,048 partials
-    // (BAGUA_PIPE_PREFOLD=0: every workgroup folds them itself, A/B)
-    const bool prefold = env_int("BAGUA_PIPE_PREFOLD", 1) != 0;
+    // requantised.  Every requantise needs the whole chunk's min/max, and each of its
+    // workgroups folds all pieces' partials itself.  BAGUA_PIPE_PREFOLD=1 folds them once
+    // in one workgroup first (BAGUA_PIECES_FOLDED): measured no faster -- the middle step
+    // 58.7 vs 58.9 us at p = 2, 43.4 vs 44.3 at p = 8 (profiles/r06_pipe_probe_p4_prefold.json)
+    // -- the fold is not what bounds the requantise, so it is off (A/B switch)
+    const bool prefold = env_int("BAGUA_PIPE_PREFOLD", 0) != 0;
     if (prefold) TRY2(bagua_minmax_u8_fold_piece_partials(dt, cs, sched, ws, ws_bytes, s0));
     const int rq_sched = sched | (prefold ? BAGUA_PIECES_FOLDED : 0);
     for (int q = 0; q < pieces; ++q) {
