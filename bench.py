@@ -152,6 +152,26 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06_pmc_traffic.json")
 PMC_SUMMARY_ONEBIT = os.path.join(ROOT, "profiles", "r06_pmc_traffic_onebit.json")
 
 
+# ---- the N > 1 line's wall budget (bench_allreduce `side`): every input is agreed
+# over the ranks (the budget left is the min over ranks, a probe step's time the max), so
+# every rank takes the same decisions
+def side_skipped(left_s: float, required: bool) -> bool:
+    """a side line that is not required is skipped once less than MIN_SIDE_S is left"""
+    return not required and left_s < MIN_SIDE_S
+
+
+def side_limit_s(left_s: float, required: bool) -> float:
+    """abort a side line after SIDE_TIMEOUT_S, or what is left of the budget if less (never
+    below MIN_SIDE_S); a required line keeps the full SIDE_TIMEOUT_S"""
+    return SIDE_TIMEOUT_S if required else max(MIN_SIDE_S, min(SIDE_TIMEOUT_S, left_s))
+
+
+def side_steps(left_s: float, t1_s: float, nominal: int) -> int:
+    """timed steps of a side line: as many as fit in a fifth of what is left after one probe
+    step of t1_s, between 2 and the nominal count"""
+    return max(2, min(nominal, int(0.2 * max(0.0, left_s) / max(t1_s, 1e-9))))
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -869,13 +889,13 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         nonlocal comm
         expired = []
         left = remaining_s()
-        if not required and left < MIN_SIDE_S:
+        if side_skipped(left, required):
             skipped.append(name)
             return float("nan")
 
         # test hook (BAGUA_BENCH_FAIL_SIDE=<side line>): that line's limit is 0 s, so its
         # communicator is aborted at once and the recovery below runs
-        limit = SIDE_TIMEOUT_S if required else max(MIN_SIDE_S, min(SIDE_TIMEOUT_S, left))
+        limit = side_limit_s(left, required)
         if os.environ.get("BAGUA_BENCH_FAIL_SIDE") == name:
             limit = 0.0
 
@@ -895,7 +915,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             # (t1 is the max over ranks and `left` the min, so every rank runs the same count)
             nominal = max(3, args.steps // 2)
             t1 = timed(fn, 1, 0)
-            steps = max(2, min(nominal, int(0.2 * max(0.0, left) / max(t1, 1e-9))))
+            steps = side_steps(left, t1, nominal)
             if steps < nominal:
                 side_steps[name] = steps
             res = timed(fn, steps, 0)

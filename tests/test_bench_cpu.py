@@ -91,3 +91,18 @@ def test_launch_ranks_stops_every_rank_when_one_fails(tmp_path, capsys):
     assert bench.launch_ranks(3, [], child_cmd=cmd) == 3
     assert time.time() - t0 < 60
     assert capsys.readouterr().out == ""
+
+
+def test_side_line_budget_rules():
+    """The N > 1 line's budget rules (bench.py side_skipped / side_limit_s / side_steps):
+    required lines always run with the full side limit; others are skipped below
+    MIN_SIDE_S left, aborted at what is left, and sized to a fifth of it."""
+    import bench
+    m, lim = bench.MIN_SIDE_S, bench.SIDE_TIMEOUT_S
+    assert not bench.side_skipped(-100.0, True) and bench.side_limit_s(-100.0, True) == lim
+    assert bench.side_skipped(m - 0.1, False) and not bench.side_skipped(m, False)
+    assert bench.side_limit_s(1000.0, False) == lim and bench.side_limit_s(30.0, False) == 30.0
+    assert bench.side_limit_s(m + 1, False) == m + 1 and bench.side_limit_s(1.0, False) == m
+    assert bench.side_steps(1000.0, 0.001, 25) == 25  # plenty of budget: the nominal count
+    assert bench.side_steps(100.0, 2.0, 25) == 10  # 0.2 * 100 s / 2 s
+    assert bench.side_steps(0.0, 2.0, 25) == 2 and bench.side_steps(-5.0, 0.0, 25) == 2  # never below 2
