@@ -35,7 +35,8 @@ except ImportError as _e:
 DTYPE_F32, DTYPE_F16, DTYPE_BF16, DTYPE_U8, DTYPE_I64, DTYPE_U64 = 0, 1, 2, 3, 4, 5
 COMPRESSION_NONE, COMPRESSION_MINMAX_UINT8, COMPRESSION_ONEBIT = 0, 1, 2
 # piece schedules (bagua_kernels.h): a count, optionally OR-ed with PIECES_TAPERED
-PIECES_COUNT_MASK, PIECES_TAPERED, PIECES_MULTIPATH, PIECES_FOLDED = 0xFFFF, 0x10000, 0x20000, 0x40000
+PIECES_COUNT_MASK, PIECES_TAPERED, PIECES_MULTIPATH, PIECES_FOLDED, PIECES_TABLES = (0xFFFF, 0x10000, 0x20000, 0x40000,
+                                                                                   0x80000)
 OP_SUM, OP_PROD, OP_MIN, OP_MAX, OP_AVG = 0, 1, 2, 3, 10
 
 STATUS = {0: "ok", 1: "invalid argument", 2: "workspace too small", 3: "HIP launch failed",

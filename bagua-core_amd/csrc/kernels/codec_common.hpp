@@ -19,6 +19,14 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kSubtiles = 4;       // vectors in flight per lane per tile
 constexpr int kMaxFusedChunks = 16;  // fused dequantise+reduce handles p <= 16
 
+// The fused reduce kernels' dequantisation tables in global memory (reduce.hip): `in`,
+// the p x 256 floats an earlier launch of the same op left (nullptr: build them);
+// `out`, where workgroup 0 of this launch leaves its own (nullptr: nothing written)
+struct FusedTables {
+    const float* in = nullptr;
+    float* out = nullptr;
+};
+
 // ----------------------------------------------------------------- dtypes --
 struct F32 {
     using storage = float;

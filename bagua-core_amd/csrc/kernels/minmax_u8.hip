@@ -621,11 +621,12 @@ static int fold_grid_target(int npartials) {
 int fused_blocks(int64_t cs, int per_vec);
 template <typename T>
 int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, int average, uint2* partials,
-                        int blocks, hipStream_t s, int e0, int e1);
+                        int blocks, hipStream_t s, int e0, int e1, FusedTables tb = FusedTables{});
 template <typename T>
 int dequant_reduce_quantize_impl(const uint8_t* in, size_t in_bytes, int cs, int p, int average,
                                  const uint2* partials, int npartials, uint8_t* seg, int64_t seg_bytes, int blocks,
-                                 hipStream_t s, void* final_chunk, int e0 = 0, int e1 = -1);
+                                 hipStream_t s, void* final_chunk, int e0 = 0, int e1 = -1,
+                                 const float* tab_in = nullptr);
 
 template <typename T>
 static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs, int p, void* tensor, int average,
@@ -679,7 +680,7 @@ static int reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int cs
 static bool piece_schedule_ok(int pieces) {
     const int n = pieces & BAGUA_PIECES_COUNT_MASK;
     return n >= 1 && (pieces & ~(BAGUA_PIECES_COUNT_MASK | BAGUA_PIECES_TAPERED | BAGUA_PIECES_MULTIPATH |
-                                 BAGUA_PIECES_FOLDED)) == 0;
+                                 BAGUA_PIECES_FOLDED | BAGUA_PIECES_TABLES)) == 0;
 }
 static int piece_count(int pieces) { return pieces & BAGUA_PIECES_COUNT_MASK; }
 
@@ -720,6 +721,18 @@ static int piece_blocks(int cs, int schedule, int per_vec) {
 // workspace's 256-byte tail
 static uint2* folded_slot(void* ws, int cs, int pieces) {
     return static_cast<uint2*>(ws) + (size_t)piece_count(pieces) * piece_blocks(cs, pieces, 4);
+}
+
+// the p x 256 dequantisation tables reduce piece 0 leaves for the op's later pieces and
+// requantise (BAGUA_PIECES_TABLES), after the folded slot's 256-byte tail
+constexpr size_t kPieceTablesBytes = (size_t)kMaxFusedChunks * 256 * sizeof(float);
+static float* piece_tables(void* ws, int cs, int pieces) {
+    return reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ws) +
+                                    (size_t)piece_count(pieces) * piece_blocks(cs, pieces, 4) * sizeof(uint2) + 256);
+}
+static bool tables_fit(const void* ws, size_t ws_bytes, int cs, int pieces) {
+    return ws && (const uint8_t*)piece_tables(const_cast<void*>(ws), cs, pieces) + kPieceTablesBytes <=
+                     (const uint8_t*)ws + ws_bytes;
 }
 
 // one workgroup folds n {min, max} key partials into out[0]
@@ -767,8 +780,17 @@ static int reduce_piece_impl(const uint8_t* recv, size_t recv_bytes, int cs, int
     int b, e;
     piece_range(cs, pieces, piece, &b, &e);
     S* chunk = tensor ? static_cast<S*>(tensor) + (int64_t)target * cs : nullptr;
+    // piece 0 leaves its tables in the workspace (when it has room); with
+    // BAGUA_PIECES_TABLES the later pieces copy them instead of building their own
+    FusedTables tb;
+    if (tables_fit(ws, ws_bytes, cs, pieces)) {
+        if (piece == 0) tb.out = piece_tables(ws, cs, pieces);
+        else if (pieces & BAGUA_PIECES_TABLES) tb.in = piece_tables(ws, cs, pieces);
+    } else if (pieces & BAGUA_PIECES_TABLES) {
+        return BAGUA_ERR_WORKSPACE;
+    }
     return dequant_reduce_impl<T>(recv, recv_bytes, cs, p, chunk, average,
-                                  static_cast<uint2*>(ws) + (size_t)piece * blocks, blocks, s, b, e);
+                                  static_cast<uint2*>(ws) + (size_t)piece * blocks, blocks, s, b, e, tb);
 }
 
 // Requantise piece `piece` of the own chunk straight from the p received segments:
@@ -798,9 +820,14 @@ static int reduce_requantize_piece_impl(const uint8_t* recv, size_t recv_bytes, 
     if (b == e && piece > 0) return BAGUA_OK;  // empty trailing piece: its bytes were written by the others
     const int grid = (int)std::min<int64_t>(fused_blocks(e - b, Vec<T>::N),
                                             tune_int("BAGUA_TUNE_RRQ_BLOCKS", fold_grid_target(partials)));
+    const float* tab = nullptr;  // BAGUA_PIECES_TABLES: the tables reduce piece 0 left
+    if (pieces & BAGUA_PIECES_TABLES) {
+        if (!tables_fit(ws, ws_bytes, cs, pieces)) return BAGUA_ERR_WORKSPACE;
+        tab = piece_tables(const_cast<void*>(ws), cs, pieces);
+    }
     return dequant_reduce_quantize_impl<T>(recv, recv_bytes, cs, p, average, part, partials,
                                            out + (int64_t)target * chunk_offset, chunk_offset, grid, s, nullptr, b,
-                                           e);
+                                           e, tab);
 }
 
 // requantise elements [e0, e1) of the own chunk from every piece's partials (the
@@ -1021,7 +1048,8 @@ int bagua_minmax_u8_piece_range(int chunk_size, int pieces, int piece, int* begi
 
 size_t bagua_minmax_u8_pipeline_workspace_bytes(int chunk_size, int pieces) {
     if (chunk_size < 0 || !piece_schedule_ok(pieces)) return 0;
-    return (size_t)piece_count(pieces) * (size_t)piece_blocks(chunk_size, pieces, 4) * sizeof(uint2) + 256;
+    return (size_t)piece_count(pieces) * (size_t)piece_blocks(chunk_size, pieces, 4) * sizeof(uint2) + 256 +
+           kPieceTablesBytes;
 }
 
 int bagua_minmax_u8_quantize_range(int dtype, const void* input, int input_num_element, int chunk_size,

@@ -173,6 +173,14 @@ __device__ __forceinline__ void build_luts(const uint8_t* in, int64_t chunk_offs
     __syncthreads();
 }
 
+// the p dequantisation tables of an earlier launch of the same op (every piece of one op
+// dequantises the same p segment headers): copied from `tab` into LDS instead of p x 256
+// correctly rounded divisions per workgroup
+__device__ __forceinline__ void load_luts(const float* __restrict__ tab, int p, float (*lut)[256]) {
+    for (int i = threadIdx.x; i < p * 256; i += kBlock) lut[i >> 8][i & 255] = tab[i];
+    __syncthreads();
+}
+
 // The reduced chunk, tile by tile: every full 16-B vector v of the result goes
 // to vec(v, packed T vector), each element j of the ragged tail (< N elements,
 // workgroup 0) to tail(j, value rounded to T).  `base` = payload byte e0 of
@@ -278,10 +286,13 @@ __device__ __forceinline__ void store_block_partial(uint32_t lo, uint32_t hi, ui
 // STORE: write the reduced chunk to `out`; PARTIALS: emit the min/max partials of
 // its values as stored in T (what the requantiser reads back).  !STORE needs
 // PARTIALS: the requantise then recomputes the values (dequant_reduce_quantize_kernel).
+// tab_in: tables of an earlier launch of the op (nullptr: build them); tab_out: workgroup 0
+// leaves its tables there for the later launches (nullptr: nothing written)
 template <typename T, int BY, int AV, bool PARTIALS, bool STORE = true, int PF = 0>
 __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
     const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t e0, int64_t cs, int p,
-    typename T::storage* __restrict__ out, uint2* __restrict__ partials) {
+    typename T::storage* __restrict__ out, uint2* __restrict__ partials, const float* __restrict__ tab_in,
+    float* __restrict__ tab_out) {
     // reduces elements [e0, e0 + cs) of the chunk (`out` points at element e0)
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
@@ -289,7 +300,13 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_kernel(
     // reduce_by(p) = BY keeps p <= 2 BY: tables for 2 BY segments (4 KiB at p <= 4)
     __shared__ QParams qp[2 * BY];
     __shared__ float lut[2 * BY][256];
-    build_luts<T>(in, chunk_offset, p, qp, lut);
+    if (tab_in) {
+        load_luts(tab_in, p, lut);
+    } else {
+        build_luts<T>(in, chunk_offset, p, qp, lut);
+        if (tab_out && blockIdx.x == 0)
+            for (int i = threadIdx.x; i < p * 256; i += kBlock) tab_out[i] = lut[i >> 8][i & 255];
+    }
     uint32_t lo = min_space(T::init_max()), hi = max_space(-T::init_max());
     reduce_tiles<T, BY, AV, PF>(
         in + 32 + e0, chunk_offset, cs, p, lut,
@@ -338,7 +355,7 @@ template <typename T, int BY, int AV, int PF = 0, bool FINAL = false>
 __global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
     const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int p, const uint2* __restrict__ partials,
     int npartials, uint8_t* __restrict__ seg, int64_t seg_bytes, typename T::storage* __restrict__ final_out,
-    int64_t e0, int64_t cs_total) {
+    int64_t e0, int64_t cs_total, const float* __restrict__ tab_in) {
     using S = typename T::storage;
     constexpr int N = Vec<T>::N;
     __shared__ QParams qp[2 * BY];  // p <= 2 BY, as in dequant_reduce_kernel
@@ -354,7 +371,8 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
     __shared__ uint32_t red[2][kWavesPerBlock];
     const int w = threadIdx.x / kWave;
     if (lane_id() == 0) { red[0][w] = lo; red[1][w] = hi; }
-    build_luts<T>(in, chunk_offset, p, qp, lut);  // its barriers publish red[][] too
+    if (tab_in) load_luts(tab_in, p, lut);  // their barriers publish red[][] too
+    else build_luts<T>(in, chunk_offset, p, qp, lut);
 #pragma unroll
     for (int i = 0; i < kWavesPerBlock; ++i) { lo = min(lo, red[0][i]); hi = min(hi, red[1][i]); }
     const float mn = from_min_space(lo), mx = from_max_space(hi);  // exact in T (header, K:462-463)
@@ -407,36 +425,36 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
 
 template <typename T, int BY, int AV>
 static void launch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, int p, typename T::storage* out,
-                         uint2* partials, int blocks, hipStream_t s) {
+                         uint2* partials, int blocks, hipStream_t s, FusedTables tb) {
     // out == nullptr: partials only (the requantise recomputes the chunk)
     if (p == 1 && BY == 2) {
         if (!out)
             launch((dequant_reduce_kernel<T, 2, AV, true, false, 1>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
-                   cs, p, out, partials);
+                   cs, p, out, partials, tb.in, tb.out);
         else if (partials)
             launch((dequant_reduce_kernel<T, 2, AV, true, true, 1>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
-                   cs, p, out, partials);
+                   cs, p, out, partials, tb.in, tb.out);
         else
             launch((dequant_reduce_kernel<T, 2, AV, false, true, 1>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
-                   cs, p, out, partials);
+                   cs, p, out, partials, tb.in, tb.out);
     } else if (!out)
         launch((dequant_reduce_kernel<T, BY, AV, true, false>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0, cs, p,
-               out, partials);
+               out, partials, tb.in, tb.out);
     else if (partials)
         launch((dequant_reduce_kernel<T, BY, AV, true>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
-                           cs, p, out, partials);
+                           cs, p, out, partials, tb.in, tb.out);
     else
         launch((dequant_reduce_kernel<T, BY, AV, false>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                           e0, cs, p, out, partials);
+                           e0, cs, p, out, partials, tb.in, tb.out);
 }
 
 template <typename T, int AV>
 static void dispatch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, int p, typename T::storage* out,
-                           uint2* partials, int blocks, hipStream_t s) {
+                           uint2* partials, int blocks, hipStream_t s, FusedTables tb) {
     switch (reduce_by(p)) {  // p <= kMaxFusedChunks (16) keeps BY <= 8
-        case 2: launch_fused<T, 2, AV>(in, co, e0, cs, p, out, partials, blocks, s); break;
-        case 4: launch_fused<T, 4, AV>(in, co, e0, cs, p, out, partials, blocks, s); break;
-        default: launch_fused<T, 8, AV>(in, co, e0, cs, p, out, partials, blocks, s); break;
+        case 2: launch_fused<T, 2, AV>(in, co, e0, cs, p, out, partials, blocks, s, tb); break;
+        case 4: launch_fused<T, 4, AV>(in, co, e0, cs, p, out, partials, blocks, s, tb); break;
+        default: launch_fused<T, 8, AV>(in, co, e0, cs, p, out, partials, blocks, s, tb); break;
     }
 }
 
@@ -448,19 +466,19 @@ struct RqRange {
 template <typename T, int AV, int PF, bool FINAL>
 static void launch_reduce_quantize(int by, const uint8_t* in, int64_t co, RqRange r, int p, const uint2* partials,
                                    int npartials, uint8_t* seg, int64_t seg_bytes, typename T::storage* final_out,
-                                   int blocks, hipStream_t s) {
+                                   int blocks, hipStream_t s, const float* tab_in) {
     switch (by) {
         case 2:
             launch((dequant_reduce_quantize_kernel<T, 2, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                   r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs);
+                   r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs, tab_in);
             break;
         case 4:
             launch((dequant_reduce_quantize_kernel<T, 4, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                   r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs);
+                   r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs, tab_in);
             break;
         default:
             launch((dequant_reduce_quantize_kernel<T, 8, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                   r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs);
+                   r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs, tab_in);
             break;
     }
 }
@@ -468,22 +486,22 @@ static void launch_reduce_quantize(int by, const uint8_t* in, int64_t co, RqRang
 template <typename T, int AV>
 static void dispatch_reduce_quantize(const uint8_t* in, int64_t co, RqRange r, int p, const uint2* partials,
                                      int npartials, uint8_t* seg, int64_t seg_bytes, typename T::storage* final_out,
-                                     int blocks, hipStream_t s) {
+                                     int blocks, hipStream_t s, const float* tab_in) {
     if (p == 1) {  // one segment: the BY = 2 tree with p known (no duplicate loads)
         if (final_out)
             launch_reduce_quantize<T, AV, 1, true>(2, in, co, r, p, partials, npartials, seg, seg_bytes, final_out,
-                                                   blocks, s);
+                                                   blocks, s, tab_in);
         else
             launch_reduce_quantize<T, AV, 1, false>(2, in, co, r, p, partials, npartials, seg, seg_bytes, nullptr,
-                                                    blocks, s);
+                                                    blocks, s, tab_in);
         return;
     }
     if (final_out)
         launch_reduce_quantize<T, AV, 0, true>(reduce_by(p), in, co, r, p, partials, npartials, seg, seg_bytes,
-                                               final_out, blocks, s);
+                                               final_out, blocks, s, tab_in);
     else
         launch_reduce_quantize<T, AV, 0, false>(reduce_by(p), in, co, r, p, partials, npartials, seg, seg_bytes,
-                                                nullptr, blocks, s);
+                                                nullptr, blocks, s, tab_in);
 }
 
 int fused_blocks(int64_t cs, int per_vec) {
@@ -494,7 +512,7 @@ int fused_blocks(int64_t cs, int per_vec) {
 
 template <typename T>
 int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void* out, int average,
-                        uint2* partials, int blocks, hipStream_t s, int e0, int e1) {
+                        uint2* partials, int blocks, hipStream_t s, int e0, int e1, FusedTables tb) {
     // reduces elements [e0, e1) of the chunk whose element 0 is at `out`;
     // out == nullptr: partials only (nothing stored)
     using S = typename T::storage;
@@ -508,9 +526,9 @@ int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void*
     const bool aligned = ((uintptr_t)o % 16 == 0) && (((uintptr_t)in + 32 + e0) % N == 0) && (co % N == 0);
     if (!aligned) return BAGUA_ERR_UNSUPPORTED;  // caller falls back to decompress + reduce
     switch (avg_mode(average, p)) {
-        case 0: dispatch_fused<T, 0>(in, co, e0, e1 - e0, p, o, partials, blocks, s); break;
-        case 1: dispatch_fused<T, 1>(in, co, e0, e1 - e0, p, o, partials, blocks, s); break;
-        default: dispatch_fused<T, 2>(in, co, e0, e1 - e0, p, o, partials, blocks, s); break;
+        case 0: dispatch_fused<T, 0>(in, co, e0, e1 - e0, p, o, partials, blocks, s, tb); break;
+        case 1: dispatch_fused<T, 1>(in, co, e0, e1 - e0, p, o, partials, blocks, s, tb); break;
+        default: dispatch_fused<T, 2>(in, co, e0, e1 - e0, p, o, partials, blocks, s, tb); break;
     }
     return check_launch();
 }
@@ -522,7 +540,7 @@ int dequant_reduce_impl(const uint8_t* in, size_t in_bytes, int cs, int p, void*
 template <typename T>
 int dequant_reduce_quantize_impl(const uint8_t* in, size_t in_bytes, int cs, int p, int average,
                                  const uint2* partials, int npartials, uint8_t* seg, int64_t seg_bytes, int blocks,
-                                 hipStream_t s, void* final_chunk, int e0, int e1) {
+                                 hipStream_t s, void* final_chunk, int e0, int e1, const float* tab_in) {
     using S = typename T::storage;
     if (e1 < 0) e1 = cs;
     if (!in || !partials || (!seg && !final_chunk) || cs < 0 || p <= 0 || npartials < 1 || e0 < 0 || e1 < e0 ||
@@ -538,22 +556,25 @@ int dequant_reduce_quantize_impl(const uint8_t* in, size_t in_bytes, int cs, int
     S* const fo = static_cast<S*>(final_chunk);
     const RqRange r{e0, (int64_t)e1 - e0, cs};
     switch (avg_mode(average, p)) {
-        case 0: dispatch_reduce_quantize<T, 0>(in, co, r, p, partials, npartials, seg, seg_bytes, fo, blocks, s); break;
-        case 1: dispatch_reduce_quantize<T, 1>(in, co, r, p, partials, npartials, seg, seg_bytes, fo, blocks, s); break;
-        default: dispatch_reduce_quantize<T, 2>(in, co, r, p, partials, npartials, seg, seg_bytes, fo, blocks, s); break;
+        case 0: dispatch_reduce_quantize<T, 0>(in, co, r, p, partials, npartials, seg, seg_bytes, fo, blocks, s, tab_in); break;
+        case 1: dispatch_reduce_quantize<T, 1>(in, co, r, p, partials, npartials, seg, seg_bytes, fo, blocks, s, tab_in); break;
+        default: dispatch_reduce_quantize<T, 2>(in, co, r, p, partials, npartials, seg, seg_bytes, fo, blocks, s, tab_in); break;
     }
     return check_launch();
 }
 
-template int dequant_reduce_impl<F32>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
-template int dequant_reduce_impl<F16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
-template int dequant_reduce_impl<BF16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int);
+template int dequant_reduce_impl<F32>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int,
+                                      FusedTables);
+template int dequant_reduce_impl<F16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int, int,
+                                      FusedTables);
+template int dequant_reduce_impl<BF16>(const uint8_t*, size_t, int, int, void*, int, uint2*, int, hipStream_t, int,
+                                       int, FusedTables);
 template int dequant_reduce_quantize_impl<F32>(const uint8_t*, size_t, int, int, int, const uint2*, int, uint8_t*,
-                                               int64_t, int, hipStream_t, void*, int, int);
+                                               int64_t, int, hipStream_t, void*, int, int, const float*);
 template int dequant_reduce_quantize_impl<F16>(const uint8_t*, size_t, int, int, int, const uint2*, int, uint8_t*,
-                                               int64_t, int, hipStream_t, void*, int, int);
+                                               int64_t, int, hipStream_t, void*, int, int, const float*);
 template int dequant_reduce_quantize_impl<BF16>(const uint8_t*, size_t, int, int, int, const uint2*, int, uint8_t*,
-                                                int64_t, int, hipStream_t, void*, int, int);
+                                                int64_t, int, hipStream_t, void*, int, int, const float*);
 
 }  // namespace bagua
 
@@ -578,13 +599,13 @@ int bagua_minmax_u8_decompress_reduce(int dtype, const uint8_t* input, size_t in
     switch (dtype) {
         case BAGUA_DTYPE_F32:
             return dequant_reduce_impl<F32>(input, input_bytes, chunk_size, num_chunks, output, average, nullptr,
-                                            fused_blocks(chunk_size, 4), s, 0, chunk_size);
+                                            fused_blocks(chunk_size, 4), s, 0, chunk_size, FusedTables{});
         case BAGUA_DTYPE_F16:
             return dequant_reduce_impl<F16>(input, input_bytes, chunk_size, num_chunks, output, average, nullptr,
-                                            fused_blocks(chunk_size, 8), s, 0, chunk_size);
+                                            fused_blocks(chunk_size, 8), s, 0, chunk_size, FusedTables{});
         case BAGUA_DTYPE_BF16:
             return dequant_reduce_impl<BF16>(input, input_bytes, chunk_size, num_chunks, output, average, nullptr,
-                                             fused_blocks(chunk_size, 8), s, 0, chunk_size);
+                                             fused_blocks(chunk_size, 8), s, 0, chunk_size, FusedTables{});
     }
     return BAGUA_ERR_UNSUPPORTED;
 }

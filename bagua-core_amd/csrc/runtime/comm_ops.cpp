@@ -573,9 +573,13 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
     // BAGUA_PIPE_RECOMPUTE=0 / 1 forces either (A/B).
     const int rc_env = env_int("BAGUA_PIPE_RECOMPUTE", -1);
     const bool recompute = rc_env >= 0 ? rc_env != 0 : 2 * (size_t)p <= bagua_dtype_bytes(dt);
+    // every piece dequantises the same p segment headers: reduce piece 0 leaves its tables
+    // in the workspace and the later pieces (and the recompute requantise) copy them
+    // (BAGUA_PIECES_TABLES; BAGUA_PIPE_TABLES=0: every launch builds its own, A/B)
+    const int tsched = sched | (env_int("BAGUA_PIPE_TABLES", 1) != 0 ? BAGUA_PIECES_TABLES : 0);
     for (int q = 0; q < pieces; ++q) {
         HIP2(hipStreamWaitEvent(s0, exchanged[q], 0));
-        TRY2(bagua_minmax_u8_reduce_piece(dt, rb, k.S, cs, p, recompute ? nullptr : x, average, k.rank, sched, q, ws,
+        TRY2(bagua_minmax_u8_reduce_piece(dt, rb, k.S, cs, p, recompute ? nullptr : x, average, k.rank, tsched, q, ws,
                                           ws_bytes, s0));
     }
     // requantise piece by piece, so the allgather of piece q starts while piece q+1 is
@@ -586,7 +590,7 @@ int centralized_pipelined(BaguaSingleCommunicatorC* c, const bagua_tensor_t* t, 
     // -- the fold is not what bounds the requantise, so it is off (A/B switch)
     const bool prefold = env_int("BAGUA_PIPE_PREFOLD", 0) != 0;
     if (prefold) TRY2(bagua_minmax_u8_fold_piece_partials(dt, cs, sched, ws, ws_bytes, s0));
-    const int rq_sched = sched | (prefold ? BAGUA_PIECES_FOLDED : 0);
+    const int rq_sched = tsched | (prefold ? BAGUA_PIECES_FOLDED : 0);
     for (int q = 0; q < pieces; ++q) {
         if (recompute)
             TRY2(bagua_minmax_u8_reduce_requantize_piece(dt, rb, k.S, cs, p, average, sb, k.S, k.rank, rq_sched, q, ws,

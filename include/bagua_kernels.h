@@ -246,6 +246,11 @@ int bagua_onebit_centralized_one_rank(int dtype, void* tensor, int num_elem, int
 /* requantise calls only: every piece's min/max partials were already folded into one
  * (bagua_minmax_u8_fold_piece_partials), so each requantise workgroup reads one value */
 #define BAGUA_PIECES_FOLDED 0x40000
+/* reduce / requantise piece calls of one op: bagua_minmax_u8_reduce_piece(piece 0) leaves
+ * the p x 256 dequantisation tables in the workspace; with this bit the later pieces and
+ * bagua_minmax_u8_reduce_requantize_piece copy them instead of recomputing them (piece 0
+ * must have run first on the same workspace and received segments) */
+#define BAGUA_PIECES_TABLES 0x80000
 int bagua_minmax_u8_piece_range(int chunk_size, int pieces, int piece, int* begin, int* end);
 size_t bagua_minmax_u8_pipeline_workspace_bytes(int chunk_size, int pieces);
 int bagua_minmax_u8_quantize_range(int dtype, const void* input, int input_num_element, int chunk_size,

@@ -17,6 +17,7 @@ pytestmark = pytest.mark.gpu
 
 F32, F16, BF16 = 0, 1, 2
 PIECES_FOLDED = 0x40000  # bagua_kernels.h BAGUA_PIECES_FOLDED
+PIECES_TABLES = 0x80000  # bagua_kernels.h BAGUA_PIECES_TABLES
 STORAGE = {F32: np.float32, F16: np.float16, BF16: np.uint16}
 TORCH = {F32: torch.float32, F16: torch.float16, BF16: torch.bfloat16}
 
@@ -338,14 +339,22 @@ def test_minmax_piecewise_building_blocks(bc, oracle_c, dtype, p, pieces):
     # requantised straight from the received segments (tensor untouched), same bytes
     recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces, ws, send_want, t_untouched=True)
     recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces, ws, send_want, prefold=True)
+    # as the op runs it: later pieces and the requantise copy piece 0's tables
+    recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces | PIECES_TABLES, ws, send_want)
     if pieces >= 3:  # the tapered schedule (first and last piece half size)
         recompute_middle(K, dtype, recv_d, S, cs, p, r, pieces | bc._native.PIECES_TAPERED, ws, send_want)
-    # the storing pair with the partials folded once (PIECES_FOLDED)
+    # the storing pair with the partials folded once (PIECES_FOLDED) and piece 0's tables
+    # copied by the later pieces (PIECES_TABLES)
     t2 = torch.zeros(p * cs, dtype=TORCH[dtype], device="cuda")
     send2 = torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
     for q in range(pieces):
-        assert K.bagua_minmax_u8_reduce_piece(dtype, recv_d.data_ptr(), S, cs, p, t2.data_ptr(), 1, r, pieces, q,
-                                              ws.data_ptr(), ws.numel(), None) == 0
+        assert K.bagua_minmax_u8_reduce_piece(dtype, recv_d.data_ptr(), S, cs, p, t2.data_ptr(), 1, r,
+                                              pieces | PIECES_TABLES, q, ws.data_ptr(), ws.numel(), None) == 0
+    t2_want = np.zeros(p * cs, STORAGE[dtype])
+    oracle_c.decompress_minmax_u8(recv, p, t2_want, dtype)
+    oracle_c.reduce_chunks(t2_want, dtype, p, r, True)
+    assert_float_bits_equal(to_host(t2, dtype)[r * cs:(r + 1) * cs], t2_want[r * cs:(r + 1) * cs], dtype,
+                            "reduced chunk with copied tables")
     assert K.bagua_minmax_u8_fold_piece_partials(dtype, cs, pieces, ws.data_ptr(), ws.numel(), None) == 0
     for q in range(pieces):
         assert K.bagua_minmax_u8_requantize_piece(dtype, t2.data_ptr(), cs, p, send2.data_ptr(), S, r,

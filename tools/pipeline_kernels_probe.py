@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--pieces", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--tapered", action="store_true", help="first and last piece half size (PIECES_TAPERED)")
+    ap.add_argument("--no-tables", action="store_true",
+                    help="every reduce / requantise piece builds its own tables (the op copies piece 0's)")
     a = ap.parse_args()
     from bagua_core import _native as N
     K = N.K
@@ -35,7 +37,7 @@ def main():
     x = torch.randn(n, device=dev, generator=g) * 1e-3
     st = torch.cuda.current_stream()
     sp = ctypes.c_void_p(st.cuda_stream)
-    out = {"bucket_bytes": 4 * n, "pieces": a.pieces, "tapered": a.tapered}
+    out = {"bucket_bytes": 4 * n, "pieces": a.pieces, "tapered": a.tapered, "tables": not a.no_tables}
 
     def timed(call):
         ts = []
@@ -54,6 +56,8 @@ def main():
         cs = n // p
         P = a.pieces
         SCH = P | (N.PIECES_TAPERED if a.tapered else 0)  # the piece schedule every piece call takes
+        if not a.no_tables:  # as the op: reduce piece 0 leaves its tables, the later pieces copy them
+            SCH |= N.PIECES_TABLES
         S = K.bagua_minmax_u8_compressed_bytes(0, cs, p)
         wsb = max(K.bagua_minmax_u8_workspace_bytes(cs, p), K.bagua_minmax_u8_pipeline_workspace_bytes(cs, SCH))
         send = torch.empty(S, dtype=torch.uint8, device=dev)
