@@ -867,7 +867,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
 
     side_errors = {}
     skipped = []  # side lines not started because the line's wall budget was spent
-    side_steps = {}  # side lines timed over fewer steps than usual to fit the budget
+    sized_steps = {}  # side lines timed over fewer steps than usual to fit the budget
 
     def remaining_s() -> float:
         # the line's wall budget left, the same on every rank (min over ranks, gloo), so
@@ -917,7 +917,7 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             t1 = timed(fn, 1, 0)
             steps = side_steps(left, t1, nominal)
             if steps < nominal:
-                side_steps[name] = steps
+                sized_steps[name] = steps
             res = timed(fn, steps, 0)
         except Exception as e:  # noqa: BLE001
             side_errors.setdefault(name, str(e)[:200])
@@ -1174,8 +1174,8 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
         extra["side_errors"] = side_errors
     extra["budget_s"] = args.budget_s
     extra["skipped_for_budget"] = skipped
-    if side_steps:
-        extra["side_steps_for_budget"] = side_steps
+    if sized_steps:
+        extra["side_steps_for_budget"] = sized_steps
     if headline_fallback:
         extra["headline_fallback"] = headline_fallback
     del comm

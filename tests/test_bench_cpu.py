@@ -106,3 +106,17 @@ def test_side_line_budget_rules():
     assert bench.side_steps(1000.0, 0.001, 25) == 25  # plenty of budget: the nominal count
     assert bench.side_steps(100.0, 2.0, 25) == 10  # 0.2 * 100 s / 2 s
     assert bench.side_steps(0.0, 2.0, 25) == 2 and bench.side_steps(-5.0, 0.0, 25) == 2  # never below 2
+
+
+def test_budget_helpers_not_shadowed():
+    """no assignment in bench.py rebinds a budget helper's name (a local dict of that name
+    once turned every N > 1 side line into a caught TypeError)"""
+    import ast
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "bench.py")) as f:
+        tree = ast.parse(f.read())
+    helpers = {"side_skipped", "side_limit_s", "side_steps"}
+    bound = [(n.id, n.lineno) for n in ast.walk(tree) if isinstance(n, ast.Name) and isinstance(n.ctx, ast.Store)
+             and n.id in helpers]
+    assert not bound, bound
