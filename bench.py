@@ -923,6 +923,9 @@ def bench_allreduce(args, world: int, rank: int, local_rank: int):
             side_errors.setdefault(name, str(e)[:200])
         finally:
             timer.cancel()
+        spend = os.environ.get("BAGUA_BENCH_SPEND", "")  # test hook "<side line>:<s>": that line takes s longer
+        if spend.partition(":")[0] == name:
+            time.sleep(float(spend.partition(":")[2] or 0))
         flag = torch.tensor([1.0 if expired else 0.0])
         if world > 1:
             dist.all_reduce(flag, op=dist.ReduceOp.MAX)
