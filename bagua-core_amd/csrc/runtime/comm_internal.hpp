@@ -54,7 +54,10 @@ int nccl_status(ncclResult_t r);
 struct ScheduleConfig {
     int32_t pieces_cap = 4;        // BAGUA_PIPELINE_PIECES: most pieces per chunk (1 disables)
     int32_t min_piece = 1 << 20;   // BAGUA_PIPELINE_MIN_PIECE: payload bytes per chunk piece
-    int32_t taper = 0;             // BAGUA_PIPELINE_TAPER=1: first/last piece half size
+    // BAGUA_PIPELINE_TAPER: first and last piece half size (from 3 pieces).  -1 (unset):
+    // the schedules an op chooses itself (the caller asked for 0 pieces) are tapered;
+    // 0: none unless the caller asks (BAGUA_PIECES_TAPERED); 1: every plain count too
+    int32_t taper = -1;
     int32_t multipath = 0;         // BAGUA_RING_MULTIPATH=1: relayed ring exchange from 6 ranks
     int32_t check = 0;             // BAGUA_CHECK_SCHEDULE=1: ranks compare op descriptors first
     int32_t reserved[3] = {0, 0, 0};

@@ -313,13 +313,20 @@ int auto_pieces(const BaguaSingleCommunicatorC* c, size_t payload_bytes) {
 }
 
 // The op's piece schedule (bagua_kernels.h: a count, optionally OR-ed with
-// BAGUA_PIECES_TAPERED): the caller's, with BAGUA_PIPELINE_TAPER=1 (the
-// communicator's ScheduleConfig, equal on every rank) tapering a count >= 3 the
-// caller left plain.  Fixed once per op and passed to every building block, so all
-// of one op's ranges agree.
+// BAGUA_PIECES_TAPERED): the caller's, tapered from 3 pieces when the communicator's
+// ScheduleConfig (equal on every rank) says so -- by default the schedules the op
+// chose itself (the caller passed 0 pieces), since round 6: at the same count the
+// first piece (quantised before any byte is on the wire) and the last one (reduced and
+// dequantised after the wire) are half size, so the unhidden codec shrinks with the same
+// number of exchange groups (1 GiB fp32, 4 pieces, one GPU's kernels: prefix 208 -> 183,
+// suffix 56 -> 38 us, profiles/r06_pipe_probe_t4.json).  BAGUA_PIPELINE_TAPER=0 keeps
+// every automatic schedule uniform, =1 tapers explicit counts too.  Fixed once per op
+// and passed to every building block, so all of one op's ranges agree.
 int op_schedule(const BaguaSingleCommunicatorC* c, int count, int caller) {
     int sched = count | (caller & BAGUA_PIECES_TAPERED);
-    if (count >= 3 && !(sched & BAGUA_PIECES_TAPERED) && c->cfg.taper) sched |= BAGUA_PIECES_TAPERED;
+    const bool automatic = (caller & BAGUA_PIECES_COUNT_MASK) == 0;
+    const bool taper = c->cfg.taper > 0 || (c->cfg.taper < 0 && automatic);
+    if (count >= 3 && !(sched & BAGUA_PIECES_TAPERED) && taper) sched |= BAGUA_PIECES_TAPERED;
     return sched;
 }
 

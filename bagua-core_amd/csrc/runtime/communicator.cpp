@@ -203,7 +203,10 @@ ScheduleConfig read_schedule_config() {
     ScheduleConfig c;
     c.pieces_cap = env_i32("BAGUA_PIPELINE_PIECES", c.pieces_cap);
     c.min_piece = env_i32("BAGUA_PIPELINE_MIN_PIECE", c.min_piece);
-    c.taper = env_i32("BAGUA_PIPELINE_TAPER", 0) == 1;
+    {  // tri-state: unset -1 (the op's automatic schedules taper), 0 never, 1 every plain count
+        const int32_t t = env_i32("BAGUA_PIPELINE_TAPER", -1);
+        c.taper = t < 0 ? -1 : (t == 1 ? 1 : 0);
+    }
     c.multipath = env_i32("BAGUA_RING_MULTIPATH", 0) != 0;
     c.check = env_i32("BAGUA_CHECK_SCHEDULE", 0) != 0;
     return c;

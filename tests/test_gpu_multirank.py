@@ -89,13 +89,16 @@ def test_centralized_low_precision_multirank(bc, oracle_c, p, dtype, cs, fused):
                                                (8, BF16, 20000, 5), (4, F16, 8192, 2), (4, F32, 1536, 4),
                                                (1, F32, 70000, 3), (16, F32, 4096 * 3, 3), (3, F32, 3 * 1024, 4),
                                                (2, F32, (1 << 21) + 1024, 0)])
-@pytest.mark.parametrize("taper", [False, True])
+@pytest.mark.parametrize("taper", ["0", "1", None])
 def test_centralized_pipelined_multirank(bc, oracle_c, p, dtype, cs, pieces, taper, monkeypatch):
     """Pieced op (side-stream exchange per piece) == the reference sequence, bit-for-bit.
     (4, F32, 1536, 4) has an empty trailing piece (pieces are 512-element aligned).
-    taper: first and last piece half size (BAGUA_PIPELINE_TAPER)."""
-    if taper:
-        monkeypatch.setenv("BAGUA_PIPELINE_TAPER", "1")
+    taper: first and last piece half size (BAGUA_PIPELINE_TAPER: 0 never, 1 every count,
+    unset -- the default -- the automatic schedules (pieces = 0) only)."""
+    if taper is None:
+        monkeypatch.delenv("BAGUA_PIPELINE_TAPER", raising=False)
+    else:
+        monkeypatch.setenv("BAGUA_PIPELINE_TAPER", taper)
     from bagua_core.communicator import loopback_communicators
     if oracle_c.minmax_compressed_size(p, cs, dtype) % p:
         pytest.skip("reference alltoall requires S % nranks == 0")
@@ -235,14 +238,17 @@ def test_decentralized_low_precision_multirank(bc, oracle_c, p, dtype, n, unfuse
 @pytest.mark.parametrize("p,dtype,n,pieces", [(2, F32, 30011, 3), (3, BF16, 70001, 4), (4, F16, 65536 + 7, 2),
                                              (8, F32, 30011, 5), (1, BF16, 40000, 3), (2, BF16, (1 << 21) + 3, 0),
                                              (3, F32, 1000, 4)])
-@pytest.mark.parametrize("taper", [False, True])
+@pytest.mark.parametrize("taper", ["0", "1", None])
 def test_decentralized_pipelined_multirank(bc, oracle_c, p, dtype, n, pieces, taper, monkeypatch):
     """Pieced ring op (quantise piece q -> send/recv piece q on the side stream -> apply piece q;
     one header travelling with piece 0) == the oracle's op simulation, all four tensors.
     (3, F32, 1000, 4): a single 512-aligned piece plus empty ones; pieces = 0: automatic.
-    taper: first and last piece half size (BAGUA_PIPELINE_TAPER)."""
-    if taper:
-        monkeypatch.setenv("BAGUA_PIPELINE_TAPER", "1")
+    taper: first and last piece half size (BAGUA_PIPELINE_TAPER: 0, 1, or unset = the
+    automatic schedules only)."""
+    if taper is None:
+        monkeypatch.delenv("BAGUA_PIPELINE_TAPER", raising=False)
+    else:
+        monkeypatch.setenv("BAGUA_PIPELINE_TAPER", taper)
     from bagua_core.communicator import loopback_communicators
     rng = np.random.default_rng(900 + p + n + pieces)
     arrs = {k: [NP.from_f32((rng.standard_normal(n) * 1e-3).astype(np.float32), dtype) for _ in range(p)]

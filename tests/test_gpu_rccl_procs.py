@@ -340,7 +340,7 @@ def test_schedule_mismatch_over_rccl(tmp_path, oracle_c):
     outs = run_procs(tmp_path, "mismatch", world, {f"x{r}": x for r, x in enumerate(xs)})
     for r, o in enumerate(outs):
         assert o["rc"].tolist() == [0, 1, 1, 0], (r, o["rc"])
-        assert o["cfg"].tolist() == [4, 1 << 20, 0, 0, 1], (r, o["cfg"])  # rank 0's switches on both
+        assert o["cfg"].tolist() == [4, 1 << 20, -1, 0, 1], (r, o["cfg"])  # rank 0's switches on both
         assert np.array_equal(o["same"], want[r].view(np.uint8)), r
         assert np.array_equal(o["after_pieces"], xs[r].view(np.uint8)), r
         assert np.array_equal(o["after_kind"], xs[r].view(np.uint8)), r

@@ -149,7 +149,8 @@ def test_schedule_env_is_read_at_creation(bc, oracle_c, monkeypatch):
     xs = _inputs(p, p * cs, 14)
     want = simulate.centralized_low_precision(oracle_c, xs, F32, True)
     comms = loopback_communicators(p, 0)
-    default = {"pieces_cap": 4, "min_piece": 1 << 20, "taper": 0, "multipath": 0, "check": 0}
+    # taper -1: the op's automatic piece schedules are tapered (round 6 default)
+    default = {"pieces_cap": 4, "min_piece": 1 << 20, "taper": -1, "multipath": 0, "check": 0}
     assert [c.schedule_config() for c in comms] == [default] * p
     monkeypatch.setenv("BAGUA_PIPELINE_TAPER", "1")
     monkeypatch.setenv("BAGUA_PIPELINE_PIECES", "8")

@@ -58,7 +58,7 @@ def test_schedule_switches_are_fixed_at_creation():
     r = subprocess.run([sys.executable, "-c", CHILD, ROOT], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
-    default = [4, 1 << 20, 0, 0, 0]
+    default = [4, 1 << 20, -1, 0, 0]  # taper -1: automatic piece schedules tapered
     assert res["first"] == [default, default]
     assert res["first_after_env_change"] == [default, default]  # fixed at creation
     assert res["second"] == [[8, 4096, 1, 1, 1]] * 3             # later communicators see the new values
