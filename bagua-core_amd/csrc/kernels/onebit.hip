@@ -503,9 +503,28 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
         } else if (i < (1 << p)) {
             const float v = p <= 4 ? lut_tree<2>(i, p, pos, neg) : lut_tree<4>(i, p, pos, neg);
             lut[0][i] = as_stored<T>(average ? v / pf : v);
+        } else if (PMAX == 2 && i < 4) {
+            lut[0][i] = 0.0f;  // p = 1: entries of a second segment that is never set (group table below)
         }
     }
     __syncthreads();
+    // p <= 2, the re-encode only (no reduced chunk stored): a lane's four elements of sub-tile
+    // k have values lut[idx_e], idx_e = bit e of the nibble k of segment 0's field | bit e of
+    // segment 1's << 1, so their part of the |x| tree, (|a0| + |a1|) + (|a2| + |a3|), is one of
+    // 256 values -- tabulated here in that order, looked up by the two nibbles -- and the sign
+    // bits of all 16 elements follow from the two fields with bitwise operations
+    __shared__ float gtab[PMAX == 2 && !STORE ? 256 : 1];
+    uint32_t negm[4] = {0, 0, 0, 0};  // all-ones where lut[idx] < 0 (the re-encoded bit of idx)
+    if constexpr (PMAX == 2 && !STORE) {
+        const int i = threadIdx.x;  // kBlock == 256: one entry per thread
+        float a[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[e] = __builtin_fabsf(lut[0][((i >> e) & 1) | (((i >> (4 + e)) & 1) << 1)]);
+        gtab[i] = (a[0] + a[1]) + (a[2] + a[3]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) negm[k] = lut[0][k] < 0.0f ? 0xffffffffu : 0u;
+        __syncthreads();
+    }
     using S = typename T::storage;
     const int lane = lane_id();
     const int64_t tiles = (cs + kObTile - 1) / kObTile;
@@ -525,6 +544,22 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
     auto process = [&](int64_t t, uint32_t (&f)[PMAX]) {
 #pragma unroll
         for (int c = 0; c < PMAX; ++c) f[c] = c < p ? f[c] : 0u;
+        if constexpr (PMAX == 2 && !STORE) {
+            if ((t + 1) * kObTile <= cs) {  // a full tile: the group table and bitwise signs
+                const uint32_t f0 = f[0], f1 = f[1];
+                const uint32_t field = ((negm[0] & ~f0 & ~f1) | (negm[1] & f0 & ~f1) | (negm[2] & ~f0 & f1) |
+                                        (negm[3] & f0 & f1)) & 0xffffu;
+                float q[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) q[k] = gtab[((f0 >> (4 * k)) & 15u) | (((f1 >> (4 * k)) & 15u) << 4)];
+                const uint32_t next = (uint32_t)__shfl_down((int)field, 1, kWave);
+                if ((lane & 1) == 0)
+                    reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane >> 1] = field | (next << 16);
+                const float sum = wave_tree_sum((q[0] + q[1]) + (q[2] + q[3]));
+                if (lane == 0) part[t] = sum;
+                return;
+            }
+        }
         float x[4][4];
         if constexpr (WIDE) {
             uint32_t re[8], ro[8], ia[16], ib[16];
