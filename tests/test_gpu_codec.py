@@ -426,6 +426,51 @@ def test_onebit_fused_reduce_requantize(bc, oracle_c, dtype, p, store):
 
 
 @pytest.mark.parametrize("dtype", [F32, F16, BF16])
+@pytest.mark.parametrize("p", [1, 2])
+@pytest.mark.parametrize("kind", ["zeros", "signed_zeros", "huge", "nan_inf", "one_side"])
+def test_onebit_fused_reduce_requantize_special(bc, oracle_c, dtype, p, kind):
+    """The p <= 2 middle step's group-table path (full tiles: a 256-entry table of each
+    sub-tile's |x| tree part, sign bits from the fields) on inputs whose reduced values are
+    +-0, overflow to +-inf, are NaN or all one sign: the same bytes as the oracle's
+    decompress + reduce_mean + compress(target)."""
+    from oracle import oracle_np as NP
+    rng = np.random.default_rng(500 + p + dtype)
+    cs = 4 * 1024 + 3  # four full tiles (the table path) and a ragged one (the per-element path)
+    base = (rng.standard_normal((p, p * cs)) * 1e-3).astype(np.float32)
+    if kind == "zeros":
+        base[:] = 0.0
+    elif kind == "signed_zeros":
+        base[:] = np.where(rng.random(base.shape) < 0.5, np.float32(-0.0), np.float32(0.0))
+    elif kind == "huge":
+        base = (np.sign(base) * np.float32(3e38)).astype(np.float32)
+        if dtype != F32:
+            base = np.sign(base).astype(np.float32) * np.float32(6e4)
+    elif kind == "nan_inf":
+        base[:, ::7] = np.inf
+        base[:, 3::11] = np.nan
+    else:
+        base = np.abs(base) + np.float32(1e-4)
+    xs = [NP.from_f32(base[r], dtype) for r in range(p)]
+    r = p - 1
+    comps = [oracle_c.compress_onebit(x, dtype, p) for x in xs]
+    S = comps[0].size
+    co = S // p
+    recv = np.concatenate([c[r * co:(r + 1) * co] for c in comps])
+    t_want = np.zeros(p * cs, STORAGE[dtype])
+    oracle_c.decompress_onebit(recv, p, t_want, dtype)
+    oracle_c.reduce_chunks(t_want, dtype, p, r, True)
+    send_want = np.zeros(S, np.uint8)
+    oracle_c.compress_onebit(t_want, dtype, p, r, out=send_want)
+    K = bc._native.K
+    recv_d = torch.from_numpy(recv).cuda()
+    send_d = torch.zeros(S, dtype=torch.uint8, device="cuda")
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
+    assert K.bagua_onebit_reduce_requantize(dtype, recv_d.data_ptr(), S, cs, p, None, 1, send_d.data_ptr(), S, r,
+                                            ws.data_ptr(), ws.numel(), None) == 0
+    assert np.array_equal(segment_bytes(send_d.cpu().numpy(), p, r), segment_bytes(send_want, p, r)), kind
+
+
+@pytest.mark.parametrize("dtype", [F32, F16, BF16])
 @pytest.mark.parametrize("p,cs,pieces,offset", [(1, 5 * 1024 + 17, 3, 0), (3, 4096, 5, 1), (2, 100000, 4, 0),
                                                 (4, 700, 2, 0)])
 def test_onebit_piecewise_building_blocks(bc, oracle_c, dtype, p, cs, pieces, offset):
