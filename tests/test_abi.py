@@ -114,7 +114,7 @@ def test_piece_ranges_cover_chunk(built):
         assert pos == cs
     assert f(10, 0, 0, ctypes.byref(b), ctypes.byref(e)) != 0
     assert f(10, 2, 2, ctypes.byref(b), ctypes.byref(e)) != 0
-    assert f(10, 2 | (1 << 18), 0, ctypes.byref(b), ctypes.byref(e)) != 0  # unknown schedule bit
+    assert f(10, 2 | (1 << 21), 0, ctypes.byref(b), ctypes.byref(e)) != 0  # unknown schedule bit
 
 
 def test_tapered_piece_schedule(built):
