@@ -480,7 +480,8 @@ __device__ __forceinline__ float lut_half(int bits, int parity, int p, const flo
     return (s[0] + s[2]) + (s[1] + s[3]);
 }
 
-// PMAX = 2: p <= 2, the index is read bit by bit; 8: the 8x8 transpose; 16: two tables
+// PMAX = 2: p <= 2, the index is read bit by bit; 4 and 8: the 8x8 transpose (4, re-encode
+// only: the pair table); 16: two tables
 template <typename T, int PMAX, bool STORE, int UT = (PMAX == 2 ? 2 : 1)>
 __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
     const uint8_t* __restrict__ in, int64_t chunk_offset, int64_t cs, int p, int average,
@@ -503,8 +504,8 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
         } else if (i < (1 << p)) {
             const float v = p <= 4 ? lut_tree<2>(i, p, pos, neg) : lut_tree<4>(i, p, pos, neg);
             lut[0][i] = as_stored<T>(average ? v / pf : v);
-        } else if (PMAX == 2 && i < 4) {
-            lut[0][i] = 0.0f;  // p = 1: entries of a second segment that is never set (group table below)
+        } else if (PMAX <= 4 && i < (1 << PMAX)) {
+            lut[0][i] = 0.0f;  // entries of segments >= p, never indexed (read by the tables below)
         }
     }
     __syncthreads();
@@ -523,6 +524,23 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
         gtab[i] = (a[0] + a[1]) + (a[2] + a[3]);
 #pragma unroll
         for (int k = 0; k < 4; ++k) negm[k] = lut[0][k] < 0.0f ? 0xffffffffu : 0u;
+        __syncthreads();
+    }
+    // 2 < p <= 4, the re-encode only: the two elements of a pair (2j, 2j + 1) take 8 bits of
+    // the four fields, so the pair's part of the |x| tree, |a0| + |a1|, and its two sign bits
+    // are one of 256 entries, looked up by an index gathered with word-wide masks (process
+    // below: bit 0 / 1 segment 0's bit of element 0 / 1, bits 2-3 segment 2's, 4-5 segment
+    // 1's, 6-7 segment 3's).  Per tile and lane that is 8 lookups and ~30 bitwise operations
+    // in place of the 8x8 transpose, 16 lookups and the per-element sign and |x| work
+    constexpr bool PAIRS = PMAX == 4 && !STORE;
+    __shared__ uint2 ptab[PAIRS ? 256 : 1];
+    if constexpr (PAIRS) {
+        const int i = threadIdx.x;  // kBlock == 256: one entry per thread
+        const int i0 = (i & 1) | ((i >> 3) & 2) | (i & 4) | ((i >> 3) & 8);
+        const int i1 = ((i >> 1) & 1) | ((i >> 4) & 2) | ((i >> 1) & 4) | ((i >> 4) & 8);
+        const float v0 = lut[0][i0], v1 = lut[0][i1];
+        ptab[i] = make_uint2(__float_as_uint(__builtin_fabsf(v0) + __builtin_fabsf(v1)),
+                             (v0 < 0.0f ? 1u : 0u) | (v1 < 0.0f ? 2u : 0u));
         __syncthreads();
     }
     using S = typename T::storage;
@@ -560,6 +578,34 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
                 return;
             }
         }
+        if constexpr (PAIRS) {
+            if ((t + 1) * kObTile <= cs) {
+                // 2-bit group g of A is segment 0's pair g (g < 8) or segment 1's (g - 8); B the same
+                // for segments 2 and 3.  Nibble m of E holds A's and B's group 2m, of O group 2m + 1;
+                // nibbles m and m + 4 together are the index of pair 2m (E) or 2m + 1 (O), m < 4
+                const uint32_t A = f[0] | (f[1] << 16), B = f[2] | (f[3] << 16);
+                const uint32_t E = (A & 0x33333333u) | ((B & 0x33333333u) << 2);
+                const uint32_t O = ((A >> 2) & 0x33333333u) | (B & 0xccccccccu);
+                // bytes 0 / 1: pairs 0 / 4 (ie), 2 / 6 (je), 1 / 5 (io), 3 / 7 (jo)
+                const uint32_t ie = (E & 0x0f0fu) | ((E >> 12) & 0xf0f0u), je = ((E >> 4) & 0x0f0fu) | ((E >> 16) & 0xf0f0u);
+                const uint32_t io = (O & 0x0f0fu) | ((O >> 12) & 0xf0f0u), jo = ((O >> 4) & 0x0f0fu) | ((O >> 16) & 0xf0f0u);
+                const uint32_t idx[8] = {ie & 255u, io & 255u, je & 255u, jo & 255u, ie >> 8, io >> 8, je >> 8, jo >> 8};
+                uint32_t field = 0;
+                float q[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {  // sub-tile k: pairs 2k and 2k + 1
+                    const uint2 a = ptab[idx[2 * k]], b = ptab[idx[2 * k + 1]];
+                    q[k] = __uint_as_float(a.x) + __uint_as_float(b.x);
+                    field |= (a.y | (b.y << 2)) << (4 * k);
+                }
+                const uint32_t next = (uint32_t)__shfl_down((int)field, 1, kWave);
+                if ((lane & 1) == 0)
+                    reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane >> 1] = field | (next << 16);
+                const float sum = wave_tree_sum((q[0] + q[1]) + (q[2] + q[3]));
+                if (lane == 0) part[t] = sum;
+                return;
+            }
+        }
         float x[4][4];
         if constexpr (WIDE) {
             uint32_t re[8], ro[8], ia[16], ib[16];
@@ -579,7 +625,7 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
         } else {
             uint32_t rows[8], ix[16];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) rows[k] = f[k];
+            for (int k = 0; k < 8; ++k) rows[k] = k < PMAX ? f[k < PMAX ? k : 0] : 0u;
             bit_columns(rows, ix);
 #pragma unroll
             for (int b = 0; b < 16; ++b) x[b / 4][b % 4] = lut[0][ix[b]];
@@ -852,21 +898,26 @@ static void launch_ob_reduce(const uint8_t* in, int64_t co, int64_t cs, int p, t
 template <typename T, int PMAX>
 static void launch_ob_reduce_lut(const uint8_t* in, int64_t co, int64_t cs, int p, int average,
                                  typename T::storage* chunk, uint8_t* seg, float* part, int blocks, hipStream_t s) {
-    if constexpr (PMAX == 2) {  // tiles per wave iteration at p <= 2: BAGUA_OB_MIDDLE_U (A/B; default 2)
-        const int u = tune_int("BAGUA_OB_MIDDLE_U", 2);
+    if constexpr (PMAX <= 4) {  // tiles per wave iteration of the re-encode: BAGUA_OB_MIDDLE_U (A/B)
+        const int u = tune_int("BAGUA_OB_MIDDLE_U", PMAX == 2 ? 2 : 1);
         if (!chunk && u == 1) {
-            launch(onebit_reduce_encode_lut_kernel<T, 2, false, 1>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
-                   average, chunk, seg, part);
+            launch(onebit_reduce_encode_lut_kernel<T, PMAX, false, 1>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs,
+                   p, average, chunk, seg, part);
+            return;
+        }
+        if (!chunk && u == 2) {
+            launch(onebit_reduce_encode_lut_kernel<T, PMAX, false, 2>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs,
+                   p, average, chunk, seg, part);
             return;
         }
         if (!chunk && u == 4) {
-            launch(onebit_reduce_encode_lut_kernel<T, 2, false, 4>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
-                   average, chunk, seg, part);
+            launch(onebit_reduce_encode_lut_kernel<T, PMAX, false, 4>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs,
+                   p, average, chunk, seg, part);
             return;
         }
         if (!chunk && u == 8) {
-            launch(onebit_reduce_encode_lut_kernel<T, 2, false, 8>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs, p,
-                   average, chunk, seg, part);
+            launch(onebit_reduce_encode_lut_kernel<T, PMAX, false, 8>, dim3(blocks), dim3(kBlock), 0, s, in, co, cs,
+                   p, average, chunk, seg, part);
             return;
         }
     }
@@ -903,6 +954,8 @@ static int ob_reduce_requantize_impl(const uint8_t* recv, size_t recv_bytes, int
         const int blocks = ob_blocks(tiles, 1, tune_int("BAGUA_TUNE_OB_MIDDLE_BLOCKS", p <= 2 ? 4096 : kTargetBlocks));
         if (p <= 2)
             launch_ob_reduce_lut<T, 2>(recv, co_in, cs, p, average, chunk, seg, part, blocks, s);
+        else if (p <= 4)
+            launch_ob_reduce_lut<T, 4>(recv, co_in, cs, p, average, chunk, seg, part, blocks, s);
         else if (p <= 8)
             launch_ob_reduce_lut<T, 8>(recv, co_in, cs, p, average, chunk, seg, part, blocks, s);
         else

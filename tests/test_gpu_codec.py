@@ -390,7 +390,7 @@ def test_onebit_goldens(bc, goldens):
 
 
 @pytest.mark.parametrize("dtype", [F32, F16, BF16])
-@pytest.mark.parametrize("p", [1, 2, 5, 8, 16])
+@pytest.mark.parametrize("p", [1, 2, 3, 4, 5, 8, 16])
 @pytest.mark.parametrize("store", [True, False])
 def test_onebit_fused_reduce_requantize(bc, oracle_c, dtype, p, store):
     """bagua_onebit_reduce_requantize == decompress_from + reduce_mean + compress(target); with a
@@ -426,11 +426,12 @@ def test_onebit_fused_reduce_requantize(bc, oracle_c, dtype, p, store):
 
 
 @pytest.mark.parametrize("dtype", [F32, F16, BF16])
-@pytest.mark.parametrize("p", [1, 2])
+@pytest.mark.parametrize("p", [1, 2, 3, 4])
 @pytest.mark.parametrize("kind", ["zeros", "signed_zeros", "huge", "nan_inf", "one_side"])
 def test_onebit_fused_reduce_requantize_special(bc, oracle_c, dtype, p, kind):
     """The p <= 2 middle step's group-table path (full tiles: a 256-entry table of each
-    sub-tile's |x| tree part, sign bits from the fields) on inputs whose reduced values are
+    sub-tile's |x| tree part, sign bits from the fields) and the 2 < p <= 4 pair-table path
+    (each element pair's |x| sum and sign bits) on inputs whose reduced values are
     +-0, overflow to +-inf, are NaN or all one sign: the same bytes as the oracle's
     decompress + reduce_mean + compress(target)."""
     from oracle import oracle_np as NP

@@ -7,7 +7,7 @@ quantise of piece 0), the middle between the last alltoall and the first allgath
 piece (reduce of the last piece + requantise of piece 0), the suffix after the last
 allgather piece (dequantise of the last piece), and the total codec time per op.
 
-    python tools/pipeline_kernels_probe.py [--pieces 4] [--reps 5]
+    python tools/pipeline_kernels_probe.py [--pieces 4] [--reps 5] [--onebit-only] [--log2n 28]
 """
 import argparse
 import ctypes
@@ -28,11 +28,13 @@ def main():
     ap.add_argument("--tapered", action="store_true", help="first and last piece half size (PIECES_TAPERED)")
     ap.add_argument("--no-tables", action="store_true",
                     help="every reduce / requantise piece builds its own tables (the op copies piece 0's)")
+    ap.add_argument("--onebit-only", action="store_true", help="the 1-bit op's kernels only")
+    ap.add_argument("--log2n", type=int, default=28, help="bucket elements (fp32), log2")
     a = ap.parse_args()
     from bagua_core import _native as N
     K = N.K
     dev = torch.device("cuda", 0)
-    n = 1 << 28
+    n = 1 << a.log2n
     g = torch.Generator(device=dev).manual_seed(3)
     x = torch.randn(n, device=dev, generator=g) * 1e-3
     st = torch.cuda.current_stream()
@@ -52,7 +54,7 @@ def main():
         ts.sort()
         return ts[len(ts) // 2]
 
-    for p in (2, 4, 8):
+    for p in (() if a.onebit_only else (2, 4, 8)):
         cs = n // p
         P = a.pieces
         SCH = P | (N.PIECES_TAPERED if a.tapered else 0)  # the piece schedule every piece call takes
