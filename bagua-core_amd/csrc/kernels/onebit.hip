@@ -103,6 +103,25 @@ __device__ __forceinline__ float wave_tree_sum(float s) {
     return s;
 }
 
+// The same tree with its result in lane 0 only (the streaming kernels store lane 0's):
+// s[l] += s[l+h] for h = 32, 16 by swapping halves across lanes (gfx950's permlane swaps),
+// h = 8..1 by DPP row shifts -- no LDS round trip per level, and 8 instructions where the
+// shuffles above take ~36 plus six ds_bpermute waits.  Every lane of the wave must be active
+__device__ __forceinline__ float wave_tree_sum_lane0(float s) {
+    s = s + __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false)[1]);
+    s = s + __uint_as_float(__builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false)[1]);
+    s = s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x108, 0xf, 0xf, false));  // row_shl:8
+    s = s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x104, 0xf, 0xf, false));  // row_shl:4
+    s = s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x102, 0xf, 0xf, false));  // row_shl:2
+    s = s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x101, 0xf, 0xf, false));  // row_shl:1
+    return s;
+}
+
+// lane l + 1's value in even lanes l (an even lane and its odd neighbour share a DPP row)
+__device__ __forceinline__ uint32_t odd_neighbour(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xf, 0xf, false);  // row_shl:1
+}
+
 // lane-local part of the tile tree for values a[sub][e]
 __device__ __forceinline__ float lane_tree(const float (&a)[4][4]) {
     float q[4];
@@ -168,14 +187,14 @@ __global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
 #pragma unroll
                 for (int e = 0; e < 4; ++e) field |= (a[u][k][e] < 0.0f ? 1u : 0u) << (k * 4 + e);
             // even lanes store their field and the odd neighbour's as one dword
-            const uint32_t next = (uint32_t)__shfl_down((int)field, 1, kWave);
+            const uint32_t next = odd_neighbour(field);
             if ((lane & 1) == 0) reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane >> 1] = field | (next << 16);
             float ab[4][4];
 #pragma unroll
             for (int k = 0; k < 4; ++k)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) ab[k][e] = __builtin_fabsf(a[u][k][e]);
-            const float s = wave_tree_sum(lane_tree(ab));
+            const float s = wave_tree_sum_lane0(lane_tree(ab));
             if (lane == 0) part[t] = s;
         }
     }
@@ -191,7 +210,8 @@ __device__ __forceinline__ float tile_from(const float* v, int64_t base, int64_t
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int64_t r = base + k * 256 + lane * 4 + e;
-            a[k][e] = r < count ? v[r] : 0.0f;
+            const float x = v[r < count ? r : count - 1];  // clamped: no load waits behind a branch
+            a[k][e] = r < count ? x : 0.0f;
         }
     return wave_tree_sum(lane_tree(a));
 }
@@ -219,12 +239,15 @@ __device__ __forceinline__ float upper_tree(int64_t m1, float (&lvl)[2][2048]) {
 
 // The fixed 1024-tree over a chunk's m1 tile partials get(r), by one
 // kObFinalizeThreads workgroup: level 1 -> 2 straight from `get` (each wave takes
-// kFinBatch groups at once and issues all their loads -- clamped, unconditional --
-// before any tree, so the pass costs one memory latency instead of one per group),
+// kFinBatch groups at once and issues all their loads before any tree, so the pass
+// costs one memory latency instead of one per group),
 // the higher levels in LDS.  Every thread returns the total (0 when m1 = 0).
 template <typename Get>
 __device__ __forceinline__ float chunk_tree(const Get& get, int64_t m1, float (&lvl)[2][2048]) {
-    const int lane = lane_id(), wave = threadIdx.x / kWave, nw = kObFinalizeThreads / kWave;
+    // the wave index through readfirstlane: the compiler then knows the group branches below
+    // are wave-uniform (scalar branches, not exec masks)
+    const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+    const int nw = kObFinalizeThreads / kWave;
     if (m1 <= 0) return 0.0f;
     int64_t m = m1;
     const int64_t g1 = (m + kObTile - 1) / kObTile;
@@ -242,15 +265,35 @@ __device__ __forceinline__ float chunk_tree(const Get& get, int64_t m1, float (&
                     for (int e = 0; e < 4; ++e) a[j][k][e] = get(bj + k * 256 + e);
             }
         } else {
+        // otherwise per group, a wave-uniform branch: a full group's loads unconditional,
+        // only the chunk's last, ragged group read element by element (guarded).  Guarded
+        // loads for the whole batch are serialised by the compiler under this workgroup's
+        // 128-VGPR budget: the finalize of 32 groups (one ragged batch) took 10.7 us, this
+        // way 4.6; of 64 (one full batch) 5.3
 #pragma unroll
-            for (int j = 0; j < kFinBatch; ++j)
+        for (int j = 0; j < kFinBatch; ++j) {
+            const int64_t g = g0 + (int64_t)j * nw;
+            const int64_t bj = g * kObTile + lane * 4;
+            if ((g + 1) * kObTile <= m) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) a[j][k][e] = get(bj + k * 256 + e);
+            } else if (g * kObTile < m) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const int64_t r = (g0 + (int64_t)j * nw) * kObTile + k * 256 + lane * 4 + e;
+                        const int64_t r = bj + k * 256 + e;
                         a[j][k][e] = r < m ? get(r) : 0.0f;
                     }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) a[j][k][e] = 0.0f;
+            }
+        }
         }
 #pragma unroll
         for (int j = 0; j < kFinBatch; ++j) {
@@ -391,14 +434,14 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_kernel(
 #pragma unroll
             for (int k = 0; k < 4; ++k) store4<T>(chunk, t * kObTile + k * 256 + lane * 4, cs, vec, x[k]);
         }
-        const uint32_t next = (uint32_t)__shfl_down((int)field, 1, kWave);
+        const uint32_t next = odd_neighbour(field);
         if ((lane & 1) == 0) reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane >> 1] = field | (next << 16);
         float ab[4][4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
             for (int e = 0; e < 4; ++e) ab[k][e] = __builtin_fabsf(x[k][e]);
-        const float sum = wave_tree_sum(lane_tree(ab));
+        const float sum = wave_tree_sum_lane0(lane_tree(ab));
         if (lane == 0) part[t] = sum;
     }
 }
@@ -570,10 +613,10 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
                 float q[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) q[k] = gtab[((f0 >> (4 * k)) & 15u) | (((f1 >> (4 * k)) & 15u) << 4)];
-                const uint32_t next = (uint32_t)__shfl_down((int)field, 1, kWave);
+                const uint32_t next = odd_neighbour(field);
                 if ((lane & 1) == 0)
                     reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane >> 1] = field | (next << 16);
-                const float sum = wave_tree_sum((q[0] + q[1]) + (q[2] + q[3]));
+                const float sum = wave_tree_sum_lane0((q[0] + q[1]) + (q[2] + q[3]));
                 if (lane == 0) part[t] = sum;
                 return;
             }
@@ -598,10 +641,10 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
                     q[k] = __uint_as_float(a.x) + __uint_as_float(b.x);
                     field |= (a.y | (b.y << 2)) << (4 * k);
                 }
-                const uint32_t next = (uint32_t)__shfl_down((int)field, 1, kWave);
+                const uint32_t next = odd_neighbour(field);
                 if ((lane & 1) == 0)
                     reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane >> 1] = field | (next << 16);
-                const float sum = wave_tree_sum((q[0] + q[1]) + (q[2] + q[3]));
+                const float sum = wave_tree_sum_lane0((q[0] + q[1]) + (q[2] + q[3]));
                 if (lane == 0) part[t] = sum;
                 return;
             }
@@ -646,14 +689,14 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
 #pragma unroll
             for (int k = 0; k < 4; ++k) store4<T>(chunk, t * kObTile + k * 256 + lane * 4, cs, vec, x[k]);
         }
-        const uint32_t next = (uint32_t)__shfl_down((int)field, 1, kWave);
+        const uint32_t next = odd_neighbour(field);
         if ((lane & 1) == 0) reinterpret_cast<uint32_t*>(bits + t * kObTileBytes)[lane >> 1] = field | (next << 16);
         float ab[4][4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
             for (int e = 0; e < 4; ++e) ab[k][e] = __builtin_fabsf(x[k][e]);
-        const float sum = wave_tree_sum(lane_tree(ab));
+        const float sum = wave_tree_sum_lane0(lane_tree(ab));
         if (lane == 0) part[t] = sum;
     };
     // U tiles per wave iteration, all their loads issued before the first is used: at
