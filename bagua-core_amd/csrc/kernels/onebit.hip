@@ -96,6 +96,13 @@ __device__ __forceinline__ void store4(typename T::storage* p, int64_t j, int64_
         if (j + e < n) p[j + e] = T::from_f(f[e]);
 }
 
+// this wave's index in the grid, through readfirstlane so the compiler knows it (and every
+// tile index and bound derived from it) is wave-uniform: scalar loop control and SGPR-based
+// addresses instead of 64-bit VALU arithmetic and exec-mask branches per tile
+__device__ __forceinline__ int64_t grid_wave() {
+    return (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+}
+
 // the 64-lane tree of the tile sum: s[l] += s[l^h], h = 32..1 (== s[l] + s[l+h])
 __device__ __forceinline__ float wave_tree_sum(float s) {
 #pragma unroll
@@ -146,7 +153,7 @@ __global__ __launch_bounds__(kBlock) void onebit_encode_kernel(
     uint8_t* bits = out + (int64_t)c * chunk_offset + 32;
     float* part = partials + (int64_t)blockIdx.y * tiles_per_chunk;
     const int lane = lane_id();
-    const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t wave = grid_wave();
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     // a lane reads 4 consecutive elements per sub-tile: 16 B for f32 but only 8 B
     // for 16-bit types, so those take TPI = 2 tiles per iteration (64 B in flight
@@ -348,7 +355,7 @@ __global__ __launch_bounds__(kBlock) void onebit_decode_kernel(const uint8_t* __
     S* dst = out + (int64_t)c * cs;
     const bool vec = ((uintptr_t)dst % (4 * sizeof(S))) == 0;
     const int lane = lane_id();
-    const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t wave = grid_wave();
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     const uint32_t sbits = __float_as_uint(scale);
     for (int64_t t = t_begin + wave; t < t_end; t += nwaves) {
@@ -390,7 +397,7 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_kernel(
     using S = typename T::storage;
     const int lane = lane_id();
     const int64_t tiles = (cs + kObTile - 1) / kObTile;
-    const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t wave = grid_wave();
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     const bool vec = ((uintptr_t)chunk % (4 * sizeof(S))) == 0;
     const float pf = (float)p;
@@ -589,7 +596,7 @@ __global__ __launch_bounds__(kBlock) void onebit_reduce_encode_lut_kernel(
     using S = typename T::storage;
     const int lane = lane_id();
     const int64_t tiles = (cs + kObTile - 1) / kObTile;
-    const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t wave = grid_wave();
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     const bool vec = ((uintptr_t)chunk % (4 * sizeof(S))) == 0;
     uint8_t* bits = out_seg + 32;
@@ -830,7 +837,7 @@ __global__ __launch_bounds__(kBlock) void onebit_one_rank_decode_kernel(const ui
     using S = typename T::storage;
     const bool vec = ((uintptr_t)out % (4 * sizeof(S))) == 0;
     const int lane = lane_id();
-    const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t wave = grid_wave();
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     const uint32_t sbits = __float_as_uint(o->scale2), mpos = o->mpos, mneg = o->mneg;
     for (int64_t t = wave; t < tiles; t += nwaves) {
