@@ -198,7 +198,12 @@ __device__ __forceinline__ void reduce_tiles(const uint8_t* base, int64_t chunk_
     const float inv = 1.0f / pf;  // exact when AV == 2
     // fast path: every segment's payload N-byte aligned (checked on host)
     const int64_t nvec = cs / N;
-    for (int64_t tile = (int64_t)blockIdx.x * kBlock * Q; tile < nvec; tile += (int64_t)gridDim.x * kBlock * Q) {
+    // a 32-bit block-tile counter from blockIdx: wave-uniform to the compiler, so the loop and
+    // the full-tile test are scalar (an int64 tile index ended up in VGPRs, with exec-mask
+    // loop control)
+    const int ntiles = (int)((nvec + (int64_t)kBlock * Q - 1) / ((int64_t)kBlock * Q));
+    for (int bt = blockIdx.x; bt < ntiles; bt += gridDim.x) {
+        const int64_t tile = (int64_t)bt * kBlock * Q;
         const bool full = tile + (int64_t)kBlock * Q <= nvec;
         float s[Q][N][BY];
 #pragma unroll
@@ -423,6 +428,17 @@ __global__ __launch_bounds__(kBlock) void dequant_reduce_quantize_kernel(
         });
 }
 
+// p = 2 known at compile time (the reduce_tiles PF parameter) for the op's recompute pair
+// (partials-only reduce + requantise, its default at p = 2 in f32): the segment loop unrolls
+// and every table row is an immediate LDS offset -- reduce 23.1 -> 18.3 us, requantise 31.6
+// -> 28.4 us per 1 GiB piece (profiles/r06_reduce_pf/).  At p = 4 / 8 the same gained
+// the recompute requantise 2 us and the storing reduce nothing, leaving the storing pair
+// the faster there, so only p = 2 is built.  BAGUA_REDUCE_PF=0: the runtime-p kernels (A/B)
+static bool pf_on() {
+    static const bool on = tune_int("BAGUA_REDUCE_PF", 1) != 0;
+    return on;
+}
+
 template <typename T, int BY, int AV>
 static void launch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, int p, typename T::storage* out,
                          uint2* partials, int blocks, hipStream_t s, FusedTables tb) {
@@ -437,10 +453,14 @@ static void launch_fused(const uint8_t* in, int64_t co, int64_t e0, int64_t cs, 
         else
             launch((dequant_reduce_kernel<T, 2, AV, false, true, 1>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
                    cs, p, out, partials, tb.in, tb.out);
-    } else if (!out)
-        launch((dequant_reduce_kernel<T, BY, AV, true, false>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0, cs, p,
-               out, partials, tb.in, tb.out);
-    else if (partials)
+    } else if (!out) {
+        if (BY == 2 && p == 2 && pf_on())  // the op's recompute reduce
+            launch((dequant_reduce_kernel<T, 2, AV, true, false, 2>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
+                   cs, p, out, partials, tb.in, tb.out);
+        else
+            launch((dequant_reduce_kernel<T, BY, AV, true, false>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
+                   cs, p, out, partials, tb.in, tb.out);
+    } else if (partials)
         launch((dequant_reduce_kernel<T, BY, AV, true>), dim3(blocks), dim3(kBlock), 0, s, in, co, e0,
                            cs, p, out, partials, tb.in, tb.out);
     else
@@ -467,19 +487,26 @@ template <typename T, int AV, int PF, bool FINAL>
 static void launch_reduce_quantize(int by, const uint8_t* in, int64_t co, RqRange r, int p, const uint2* partials,
                                    int npartials, uint8_t* seg, int64_t seg_bytes, typename T::storage* final_out,
                                    int blocks, hipStream_t s, const float* tab_in) {
-    switch (by) {
-        case 2:
-            launch((dequant_reduce_quantize_kernel<T, 2, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                   r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs, tab_in);
-            break;
-        case 4:
-            launch((dequant_reduce_quantize_kernel<T, 4, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                   r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs, tab_in);
-            break;
-        default:
-            launch((dequant_reduce_quantize_kernel<T, 8, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
-                   r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs, tab_in);
-            break;
+    if constexpr (PF > 0) {  // p known: only its own tree width (reduce_by(PF)) is built
+        constexpr int BYP = PF <= 4 ? 2 : PF <= 8 ? 4 : 8;
+        (void)by;
+        launch((dequant_reduce_quantize_kernel<T, BYP, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
+               r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs, tab_in);
+    } else {
+        switch (by) {
+            case 2:
+                launch((dequant_reduce_quantize_kernel<T, 2, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
+                       r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs, tab_in);
+                break;
+            case 4:
+                launch((dequant_reduce_quantize_kernel<T, 4, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
+                       r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs, tab_in);
+                break;
+            default:
+                launch((dequant_reduce_quantize_kernel<T, 8, AV, PF, FINAL>), dim3(blocks), dim3(kBlock), 0, s, in, co,
+                       r.len, p, partials, npartials, seg, seg_bytes, final_out, r.e0, r.cs, tab_in);
+                break;
+        }
     }
 }
 
@@ -499,6 +526,9 @@ static void dispatch_reduce_quantize(const uint8_t* in, int64_t co, RqRange r, i
     if (final_out)
         launch_reduce_quantize<T, AV, 0, true>(reduce_by(p), in, co, r, p, partials, npartials, seg, seg_bytes,
                                                final_out, blocks, s, tab_in);
+    else if (p == 2 && pf_on())  // the op's recompute requantise
+        launch_reduce_quantize<T, AV, 2, false>(2, in, co, r, p, partials, npartials, seg, seg_bytes, nullptr,
+                                                blocks, s, tab_in);
     else
         launch_reduce_quantize<T, AV, 0, false>(reduce_by(p), in, co, r, p, partials, npartials, seg, seg_bytes,
                                                 nullptr, blocks, s, tab_in);
