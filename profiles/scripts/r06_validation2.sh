@@ -3,7 +3,7 @@
 # and the 1-bit line
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r06val2
+O=gpurun_out/${VAL_DIR:-r06val2}
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gputests.log 2>&1 || exit 1
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
