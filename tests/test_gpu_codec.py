@@ -509,8 +509,12 @@ def test_onebit_piecewise_building_blocks(bc, oracle_c, dtype, p, cs, pieces, of
 
 
 @pytest.mark.parametrize("dtype", [F32, BF16])
-@pytest.mark.parametrize("p,cs,offset", [(1, 3 * 1024 * 1024 + 17, 0), (2, 1500, 1), (1, 1024 * 1100, 2)])
+@pytest.mark.parametrize("p,cs,offset", [(1, 3 * 1024 * 1024 + 17, 0), (2, 1500, 1), (1, 1024 * 1100, 2),
+                                         (1, 65 * (1 << 20) + 5 * 1024 + 3, 0), (8, 4 * (1 << 20) + 7, 0)])
 def test_onebit_vs_oracle(bc, oracle_c, dtype, p, cs, offset):
+    """The last two shapes drive the finalize's scale tree through its batch paths: 66 groups of
+    1,024 tile partials (one full batch of 64, then a batch of one full group, one ragged group
+    and empty ones) and 8 chunks of 5 groups (a ragged batch each)."""
     from oracle import oracle_np as NP
     rng = np.random.default_rng(cs + p)
     x = NP.from_f32((rng.standard_normal(p * cs) * 1e-3).astype(np.float32), dtype)
