@@ -120,6 +120,37 @@ def test_centralized_pipelined_multirank(bc, oracle_c, p, dtype, cs, pieces, tap
         assert np.array_equal(host(ts[r], dtype).view(np.uint8), want[r].view(np.uint8)), f"rank {r}"
 
 
+@pytest.mark.parametrize("p,dtype,cs,pieces", [(2, F32, 40000, 3), (2, BF16, 30000, 4), (2, F16, 8192 + 512, 2),
+                                               (4, F32, 65536, 4), (8, F32, 12345 * 4, 2)])
+@pytest.mark.parametrize("recompute", ["0", "1"])
+def test_centralized_pipelined_middle_variants(bc, oracle_c, p, dtype, cs, pieces, recompute, monkeypatch):
+    """Both middle steps of the pieced op, forced (BAGUA_PIPE_RECOMPUTE): the storing pair
+    (reduce pieces store the reduced chunk, the requantise reads it) and the recompute pair
+    (partials-only reduce pieces, the requantise recomputes the values from the received
+    segments; at p = 2 the kernels built with p known) -- every rank bit-for-bit the reference
+    sequence, in every dtype."""
+    monkeypatch.setenv("BAGUA_PIPE_RECOMPUTE", recompute)
+    from bagua_core.communicator import loopback_communicators
+    if oracle_c.minmax_compressed_size(p, cs, dtype) % p:
+        pytest.skip("reference alltoall requires S % nranks == 0")
+    rng = np.random.default_rng(p * 1300 + dtype + cs)
+    xs = [NP.from_f32((rng.standard_normal(p * cs) * 1e-3 + 0.01 * r).astype(np.float32), dtype) for r in range(p)]
+    want = simulate.centralized_low_precision(oracle_c, xs, dtype, True)
+    comms = loopback_communicators(p, 0)
+    ts = [dev(x, dtype) for x in xs]
+    torch.cuda.synchronize()
+    N = bc._native
+
+    def rank(r):
+        raw = bc.BaguaTensorPy(ts[r], f"g{r}").raw()
+        N.check(N.C.bagua_centralized_low_precision_pipelined(comms[r].handle, ctypes.byref(raw), 1,
+                                                              N.COMPRESSION_MINMAX_UINT8, pieces), f"rank {r}")
+
+    run_ranks(rank, p)
+    for r in range(p):
+        assert np.array_equal(host(ts[r], dtype).view(np.uint8), want[r].view(np.uint8)), f"rank {r}"
+
+
 @pytest.mark.parametrize("p,dtype,cs,pieces", [(2, F32, 4096 * 3, 3), (4, F32, 40000, 4), (8, BF16, 2500 * 4, 2),
                                                (8, F32, 5000 * 8, 5), (4, F16, 1024 * 7 + 3, 3), (1, F32, 70000, 3),
                                                (16, F32, 3000 * 2, 2), (3, F32, 2048, 4), (2, F32, 0, 2),
